@@ -1,0 +1,288 @@
+"""Benchmark of the MHAHeadDim64 hot path on MI355X (one JSON line on rank 0).
+
+Metric (BASELINE.json): attention-calls/sec & ms/call, 1x4x1024x1024 d=64 fp16; % MFMA peak.
+
+A step is ONE MHAHeadDim64 call — the plugin's enqueue() on a [1,4,1024,64] fp16 Q/K/V
+(BASELINE configs[1]) — exactly what the TensorRT engine does per attention node. The K timed
+steps are K independent calls captured into one hipGraph (the reference's demo also replays a
+CUDA graph, demo/lightglue_trt.cpp:347-366) and replayed once between barriers, inputs resident
+in HBM. value = calls/s over all ranks (replicas: each GPU runs its own stream of calls, no
+collective on the data path; the only collective is the max-over-ranks of the timer).
+
+Extra fields: roofline of the dominant kernel (main attention kernel; duration from HIP events
+on the launch stream), isolated single-call latency, the batched-launch throughput (several
+calls stacked in one launch) and the CPU baseline (the reference's PyTorch attention restated in
+oracle/oracle.py, timed on this host's cores on a bounded sample).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_DIR = os.path.join(REPO, "lightglue-with-flashattentionv2-tensorrt_amd")
+for _p in (REPO, PKG_DIR):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "attention-calls/sec & ms/call, 1×1024×1024 d=64 fp16; % MFMA peak"
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters): dense fp16 MFMA
+# ~2.5 PFLOP/s (not the 2:1-sparse figure), HBM3E 8 TB/s.
+PEAK_F16_TFLOPS = 2500.0
+PEAK_HBM_GBS = 8000.0
+
+
+def call_flops(b, h, nq, nkv, d=64):
+    """Algorithmic FLOPs of one call: QK^T and PV, 2 flops per MAC."""
+    return 4 * b * h * nq * nkv * d
+
+
+def call_bytes(b, h, nq, nkv, in_bytes=2, out_bytes=2, d=64):
+    return b * h * d * (nq * in_bytes + 2 * nkv * in_bytes + nq * out_bytes)
+
+
+# ----------------------------------------------------------------------------------------
+# distributed timing (replicas); testable on CPU with gloo
+# ----------------------------------------------------------------------------------------
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def timed_region(run_steps, barrier, sync, reduce_max):
+    """barrier + sync, run the K steps, sync + barrier; return max-over-ranks seconds."""
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    run_steps()
+    sync()
+    dt = time.perf_counter() - t0
+    barrier()
+    return reduce_max(dt)
+
+
+def make_collectives(torch, dist, device):
+    if dist is None or not dist.is_initialized():
+        return (lambda: None), (lambda x: x)
+
+    def barrier():
+        dist.barrier()
+
+    def reduce_max(x):
+        t = torch.tensor([x], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    return barrier, reduce_max
+
+
+# ----------------------------------------------------------------------------------------
+# GPU measurement helpers
+# ----------------------------------------------------------------------------------------
+def event_durations_ms(torch, launch, n, stream):
+    """Per-launch GPU durations from HIP events recorded on the launch stream.
+
+    A long sleep kernel is queued first so that every (event, launch, event) triple is
+    already enqueued when the GPU reaches it: the events then time the kernel(s), not
+    the host's launch latency."""
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(int(40e6))
+        for i in range(n):
+            starts[i].record(stream)
+            launch()
+            ends[i].record(stream)
+    stream.synchronize()
+    return [s.elapsed_time(e) for s, e in zip(starts, ends)]
+
+
+def cpu_baseline(seconds=10.0, nq=1024, nkv=1024):
+    """Reference PyTorch CPU attention (lightglue_pytorch_no_plugin/lightglue.py:82-84, restated
+    in oracle/oracle.py) on this host, fp32, bounded sample of ~`seconds`."""
+    import torch
+
+    from lightglue_amd import synth
+    from oracle import oracle
+
+    threads = torch.get_num_threads()
+    qn, kn, vn = synth.qkv(2, nq, nkv)
+    q, k, v = (torch.from_numpy(x) for x in (qn, kn, vn))
+    for _ in range(3):
+        oracle.attention_torch(q, k, v)
+    n = 0
+    t0 = time.perf_counter()
+    times = []
+    while time.perf_counter() - t0 < seconds:
+        t1 = time.perf_counter()
+        oracle.attention_torch(q, k, v)
+        times.append(time.perf_counter() - t1)
+        n += 1
+    med = statistics.median(times)
+    return {"value": round(1.0 / med, 2), "unit": "calls/s", "cores": threads, "kind": "port",
+            "ms_per_call": round(med * 1e3, 3),
+            "sample": f"{n} calls of 1x4x{nq}x{nkv} d=64 fp32, torch CPU matmul-softmax-matmul "
+                      f"(reference Attention.forward math), median per call, {threads} threads, ~{seconds:.0f}s"}
+
+
+def load_traffic(tag):
+    """HBM bytes per launch of the main kernel from the committed rocprofv3 PMC pass (or None)."""
+    path = os.path.join(REPO, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(tag)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--nq", type=int, default=1024)
+    ap.add_argument("--nkv", type=int, default=1024)
+    ap.add_argument("--batched", type=int, default=8, help="calls stacked per launch for the batched figure")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--quick", action="store_true", help="skip the secondary measurements (profiling runs)")
+    args = ap.parse_args()
+
+    import torch
+
+    ws, rank, local = dist_env()
+    dist = None
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=device)
+    barrier, reduce_max = make_collectives(torch, dist, device)
+
+    import lightglue_amd
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    nq, nkv = args.nq, args.nkv
+    qn, kn, vn = synth.qkv(100 + rank, nq, nkv)
+    q, k, v = (torch.from_numpy(x).to(device).half().contiguous() for x in (qn, kn, vn))
+    out = torch.empty_like(q)
+
+    stream = torch.cuda.Stream(device)
+    stream.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):                 # W untimed warmup steps
+            lightglue_amd.mha_hd64(q, k, v, out=out)
+    stream.synchronize()
+
+    # Capture the K timed steps (K independent enqueues) into one graph.
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=stream):
+        for _ in range(args.steps):
+            lightglue_amd.mha_hd64(q, k, v, out=out)
+    graph.replay()                                   # upload / first-replay cost outside the timer
+    stream.synchronize()
+
+    elapsed = timed_region(lambda: graph.replay(), barrier, lambda: torch.cuda.synchronize(device), reduce_max)
+    total_calls = args.steps * ws
+    value = total_calls / elapsed
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    import ctypes
+
+    plan_c = (ctypes.c_int32 * 3)()
+    ws_need = lib.mha_hd64_plan(1, 4, nq, nkv, 5242880, plan_c)
+    q_waves, splits, _ = list(plan_c)
+    flops = call_flops(1, 4, nq, nkv)
+    result = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "calls/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp16",
+        "data": "synthetic",
+        "config": {"workload": "MHAHeadDim64 plugin enqueue, Q/K/V [1,4,1024,64] fp16 -> O fp16 "
+                               "(BASELINE configs[1]); K independent calls per step-graph",
+                   "batch": 1, "heads": 4, "nq": nq, "nkv": nkv, "head_dim": 64,
+                   "parallelism": f"replicas{ws}", "plan": {"q_waves": q_waves, "kv_splits": splits}},
+    }
+
+    if not args.quick:
+        ws_buf = torch.empty(max(ws_need, 16), dtype=torch.uint8, device=device)
+        sp = stream.cuda_stream
+
+        def main_kernel():
+            lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), 1, 4, nq, nkv, 0,
+                                       0, q_waves, splits, ws_buf.data_ptr(), ws_buf.numel(), sp, 1)
+
+        def combine_kernel():
+            lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), 1, 4, nq, nkv, 0,
+                                       0, q_waves, splits, ws_buf.data_ptr(), ws_buf.numel(), sp, 2)
+
+        def full_call():
+            with torch.cuda.stream(stream):
+                lightglue_amd.mha_hd64(q, k, v, out=out)
+
+        t_main = statistics.mean(event_durations_ms(torch, main_kernel, 200, stream)[20:])
+        t_comb = statistics.mean(event_durations_ms(torch, combine_kernel, 200, stream)[20:]) if splits > 1 else 0.0
+        t_call = statistics.median(event_durations_ms(torch, full_call, 200, stream)[20:])
+        achieved = flops / (t_main * 1e-3) / 1e12
+        traffic = load_traffic("main_kernel_bytes_per_launch")
+        result["roofline"] = {
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": traffic,
+            "kernel": f"mha_hd64_fwd_kernel<f16,f16,QW={q_waves}> ({splits}-way KV split)",
+            "kernel_us": round(t_main * 1e3, 3), "combine_us": round(t_comb * 1e3, 3),
+            "flops_per_launch": flops, "algorithmic_bytes_per_call": call_bytes(1, 4, nq, nkv),
+        }
+        result["isolated_call_us"] = round(t_call * 1e3, 3)
+
+        # Batched launch: `batched` independent calls stacked in the batch dimension of one launch.
+        B = args.batched
+        qb, kb, vb = synth.qkv(300 + rank, nq, nkv, batch=B)
+        qb, kb, vb = (torch.from_numpy(x).to(device).half().contiguous() for x in (qb, kb, vb))
+        ob = torch.empty_like(qb)
+
+        def batched():
+            with torch.cuda.stream(stream):
+                lightglue_amd.mha_hd64_batched(qb, kb, vb, out=ob)
+
+        for _ in range(20):
+            batched()
+        tb = statistics.median(event_durations_ms(torch, batched, 100, stream)[10:])
+        result["batched"] = {
+            "calls_per_launch": B, "launch_us": round(tb * 1e3, 3),
+            "calls_per_s_per_gpu": round(B / (tb * 1e-3), 1),
+            "tflops": round(B * flops / (tb * 1e-3) / 1e12, 2),
+            "frac": round(B * flops / (tb * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
+        }
+
+    if rank == 0 and not args.no_cpu_baseline and not args.quick:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, nq, nkv)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,48 @@
+// mha_hd64_internal.h — host-side launch plumbing shared by the kernels and the plugin shim.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+namespace mha_hd64 {
+
+constexpr int kHeadDim = 64;
+constexpr int kMaxSeqLen = 2048;
+constexpr int kNumHeads = 4;
+
+enum class InType { F16, F32 };
+enum class OutType { F16, F32 };
+
+// One attention call: Q [batch, heads, nq, 64], K/V [batch, heads, nkv, 64], O like Q.
+// Contiguous row-major ("kLINEAR"), the layout the reference plugin receives
+// (lightglue_attention_plugin.cpp:122-163, head stride N*64).
+struct Call {
+    const void* q;
+    const void* k;
+    const void* v;
+    void* o;
+    int batch;
+    int heads;
+    int nq;
+    int nkv;
+};
+
+// Launch-shape choice for one call (exposed so tests/bench can force a variant).
+struct LaunchPlan {
+    int q_waves;          // waves per workgroup that own distinct 32-row query slices (1, 2 or 4)
+    int splits;           // KV split across workgroups (1 = no combine pass)
+    int tiles_per_split;  // KV super-tiles (64 * (4 / q_waves) keys) per split
+    size_t ws_needed;     // workspace bytes the plan uses
+};
+
+LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves = 0, int force_splits = 0);
+size_t split_workspace_bytes(const Call& c, int splits);
+
+// Returns hipSuccess or the launch error. phase_mask (measurement hook): bit 0 = main
+// kernel, bit 1 = split-KV combine kernel.
+hipError_t launch_attention(const Call& c, InType in, OutType out, void* workspace, size_t ws_bytes,
+                            hipStream_t stream, int force_q_waves = 0, int force_splits = 0,
+                            int phase_mask = 3);
+
+}  // namespace mha_hd64

@@ -1,0 +1,151 @@
+"""ctypes binding of the C ABI in include/mha_hd64.h (lib/libmha_hd64.so).
+
+This is the reference-side binding a Python host adds in place of TensorRT's
+``trtexec --plugins=liblightglue_attention_plugin.so`` / ``dlopen`` (steps.txt:135-179,
+demo/lightglue_trt.cpp:15). The library is built in-tree by ``make`` in the package
+directory (``__graft_entry__.build()``); there is deliberately no fallback: if the
+shared library is missing, ``load()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libmha_hd64.so")
+
+DT_FLOAT = 0  # nvinfer1::DataType::kFLOAT
+DT_HALF = 1   # nvinfer1::DataType::kHALF
+FMT_LINEAR = 0  # nvinfer1::TensorFormat::kLINEAR
+
+STATUS_SUCCESS = 0
+STATUS_BAD_PARAM = 1
+STATUS_LAUNCH_FAILED = 2
+STATUS_WORKSPACE = 3
+
+BATCH = 1
+NUM_HEADS = 4
+MAX_SEQ_LEN = 2048
+HEAD_DIM = 64
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [("nb_dims", ctypes.c_int32), ("d", ctypes.c_int64 * 8)]
+
+    @classmethod
+    def of(cls, shape) -> "Dims":
+        shape = tuple(int(x) for x in shape)
+        d = cls()
+        d.nb_dims = len(shape)
+        for i, x in enumerate(shape):
+            d.d[i] = x
+        return d
+
+    def shape(self):
+        return tuple(int(self.d[i]) for i in range(self.nb_dims))
+
+
+class TensorDesc(ctypes.Structure):
+    _fields_ = [("dims", Dims), ("type", ctypes.c_int32), ("format", ctypes.c_int32), ("scale", ctypes.c_float)]
+
+    @classmethod
+    def of(cls, shape, dtype: int, fmt: int = FMT_LINEAR) -> "TensorDesc":
+        t = cls()
+        t.dims = Dims.of(shape)
+        t.type = dtype
+        t.format = fmt
+        t.scale = 1.0
+        return t
+
+
+class DynamicTensorDesc(ctypes.Structure):
+    _fields_ = [("desc", TensorDesc), ("min", Dims), ("max", Dims)]
+
+    @classmethod
+    def of(cls, shape, dtype: int, fmt: int = FMT_LINEAR) -> "DynamicTensorDesc":
+        t = cls()
+        t.desc = TensorDesc.of(shape, dtype, fmt)
+        t.min = Dims.of(shape)
+        t.max = Dims.of(shape)
+        return t
+
+
+# Every symbol include/mha_hd64.h declares, with its ctypes signature.
+_P = ctypes.c_void_p
+_I = ctypes.c_int32
+_S = ctypes.c_size_t
+_C = ctypes.c_char_p
+SIGNATURES = {
+    "mha_hd64_creator_plugin_name": ([], _C),
+    "mha_hd64_creator_plugin_version": ([], _C),
+    "mha_hd64_creator_nb_fields": ([], _I),
+    "mha_hd64_create_plugin": ([_C], _P),
+    "mha_hd64_deserialize_plugin": ([_C, _P, _S], _P),
+    "mha_hd64_destroy": ([_P], None),
+    "mha_hd64_clone": ([_P], _P),
+    "mha_hd64_initialize": ([_P], _I),
+    "mha_hd64_terminate": ([_P], None),
+    "mha_hd64_get_serialization_size": ([_P], _S),
+    "mha_hd64_serialize": ([_P, _P], None),
+    "mha_hd64_get_plugin_type": ([_P], _C),
+    "mha_hd64_get_plugin_version": ([_P], _C),
+    "mha_hd64_set_plugin_namespace": ([_P, _C], None),
+    "mha_hd64_get_plugin_namespace": ([_P], _C),
+    "mha_hd64_attach_to_context": ([_P], None),
+    "mha_hd64_detach_from_context": ([_P], None),
+    "mha_hd64_get_nb_outputs": ([_P], _I),
+    "mha_hd64_get_output_dimensions": ([_P, _I, ctypes.POINTER(Dims), _I, ctypes.POINTER(Dims)], _I),
+    "mha_hd64_supports_format_combination": ([_P, _I, ctypes.POINTER(TensorDesc), _I, _I], _I),
+    "mha_hd64_get_output_data_type": ([_P, _I, ctypes.POINTER(ctypes.c_int32), _I, ctypes.POINTER(ctypes.c_int32)], _I),
+    "mha_hd64_configure_plugin": ([_P, ctypes.POINTER(DynamicTensorDesc), _I, ctypes.POINTER(DynamicTensorDesc), _I], _I),
+    "mha_hd64_get_workspace_size": ([_P, ctypes.POINTER(TensorDesc), _I, ctypes.POINTER(TensorDesc), _I], _S),
+    "mha_hd64_enqueue": ([_P, ctypes.POINTER(TensorDesc), ctypes.POINTER(TensorDesc),
+                          ctypes.POINTER(_P), ctypes.POINTER(_P), _P, _P], _I),
+    "mha_hd64_launch_fp16in_fp16out": ([_P, _P, _P, _P, _I, _I, _I, _I, _P, _S, _P], _I),
+    "mha_hd64_launch_fp16in_fp32out": ([_P, _P, _P, _P, _I, _I, _I, _I, _P, _S, _P], _I),
+    "mha_hd64_launch_fp32in_fp32out": ([_P, _P, _P, _P, _I, _I, _I, _I, _P, _S, _P], _I),
+    "mha_hd64_launch_workspace_bytes": ([_I, _I, _I, _I], _S),
+    "mha_hd64_last_error": ([], _C),
+    "mha_hd64_set_abort_on_error": ([_I], None),
+    "mha_hd64_build_info": ([], _C),
+}
+# Test/bench hooks exported by the library but not part of the public header.
+HOOKS = {
+    "mha_hd64_launch_forced": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _S, _P, _I], _I),
+    "mha_hd64_plan": ([_I, _I, _I, _I, _S, ctypes.POINTER(ctypes.c_int32)], _S),
+}
+
+_lib = None
+
+
+class LibraryMissing(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load lib/libmha_hd64.so (build it with __graft_entry__.build()). Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise LibraryMissing(
+            f"{LIB_PATH} not found: the MI355X HIP extension is not built "
+            "(run `python -c 'import __graft_entry__ as g; g.build()'` or `make -C "
+            f"{PKG_DIR}`). There is no CPU fallback.")
+    try:  # bind to the HIP runtime torch already loaded, if torch is in use
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover
+        pass
+    lib = ctypes.CDLL(LIB_PATH)
+    for table in (SIGNATURES, HOOKS):
+        for name, (args, res) in table.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    msg = load().mha_hd64_last_error()
+    return msg.decode() if msg else ""

@@ -1,0 +1,253 @@
+"""C-ABI boundary tests that need no GPU: the library loads, exports every symbol that
+include/mha_hd64.h declares, and the plugin's host-side contract mirrors the reference
+(lightglue_attention_plugin/lightglue_attention_plugin.cpp:28-422)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "mha_hd64.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mha_hd64_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from lightglue_amd import _lib
+
+    return _lib.load()
+
+
+@pytest.fixture()
+def plugin():
+    from lightglue_amd import LightGlueAttentionPlugin
+
+    p = LightGlueAttentionPlugin()
+    yield p
+    p.destroy()
+
+
+def desc(shape, dt=1, fmt=0):
+    from lightglue_amd._lib import TensorDesc
+
+    return TensorDesc.of(shape, dt, fmt)
+
+
+def dyn(shape, dt=1, fmt=0):
+    from lightglue_amd._lib import DynamicTensorDesc
+
+    return DynamicTensorDesc.of(shape, dt, fmt)
+
+
+def test_every_header_symbol_is_exported(lib):
+    from lightglue_amd import _lib
+
+    names = header_functions()
+    assert len(names) >= 30
+    for n in names:
+        assert hasattr(lib, n), n
+        assert n in _lib.SIGNATURES, f"{n} has no ctypes signature"
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (mha_hd64_\w+)", out))
+    assert set(names) <= exported
+
+
+def test_library_is_gfx950_code_object(lib):
+    from lightglue_amd import _lib
+
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data, "no gfx950 code object in the fat binary"
+    assert b"gfx950" in ctypes.string_at(lib.mha_hd64_build_info())
+
+
+def test_identity(plugin):
+    from lightglue_amd import LightGlueAttentionPluginCreator
+
+    c = LightGlueAttentionPluginCreator()
+    assert c.get_plugin_name() == "MHAHeadDim64" and c.get_plugin_version() == "1"
+    assert c.get_field_names() == []
+    assert plugin.get_plugin_type() == "MHAHeadDim64" and plugin.get_plugin_version() == "1"
+    assert plugin.get_plugin_namespace() == ""
+    plugin.set_plugin_namespace("ns")
+    assert plugin.get_plugin_namespace() == "ns"
+    assert plugin.clone().get_plugin_namespace() == "ns"
+    assert plugin.get_nb_outputs() == 1
+    assert plugin.initialize() == 0
+    assert plugin.get_serialization_size() == 0 and plugin.serialize() == b""
+    p2 = c.deserialize_plugin("MHAHeadDim64", b"")
+    assert p2.get_plugin_type() == "MHAHeadDim64"
+    plugin.attach_to_context()
+    plugin.detach_from_context()
+
+
+def test_output_dimensions(plugin):
+    from lightglue_amd import PluginError
+
+    assert plugin.get_output_dimensions(0, [(1, 4, 100, 64), (1, 4, 77, 64), (1, 4, 77, 64)]) == (1, 4, 100, 64)
+    with pytest.raises(PluginError):
+        plugin.get_output_dimensions(1, [(1, 4, 100, 64)] * 3)
+    with pytest.raises(PluginError):
+        plugin.get_output_dimensions(0, [(1, 4, 100, 64)] * 2)
+    with pytest.raises(PluginError):
+        plugin.get_output_dimensions(0, [(4, 100, 64), (1, 4, 1, 64), (1, 4, 1, 64)])
+
+
+def test_output_data_type(plugin):
+    assert plugin.get_output_data_type(0, [1, 1, 1]) == 1
+    assert plugin.get_output_data_type(0, [0, 0, 0]) == 0
+
+
+def test_supports_format_combination(plugin):
+    from lightglue_amd import PluginError
+
+    half = [desc((1, 4, 8, 64), 1)] * 4
+    flt = [desc((1, 4, 8, 64), 0)] * 4
+    for pos in range(4):
+        assert plugin.supports_format_combination(pos, half, 3, 1)
+        assert plugin.supports_format_combination(pos, flt, 3, 1)
+    mixed = [desc((1, 4, 8, 64), 1), desc((1, 4, 8, 64), 0), desc((1, 4, 8, 64), 1), desc((1, 4, 8, 64), 1)]
+    assert not plugin.supports_format_combination(1, mixed, 3, 1)
+    int8 = [desc((1, 4, 8, 64), 2)] + half[1:]
+    assert not plugin.supports_format_combination(0, int8, 3, 1)
+    chw = [desc((1, 4, 8, 64), 1, fmt=1)] + half[1:]
+    assert not plugin.supports_format_combination(0, chw, 3, 1)
+    with pytest.raises(PluginError):
+        plugin.supports_format_combination(4, half, 3, 1)
+
+
+def test_workspace_size_is_fixed(plugin):
+    for n in (1, 64, 1000, 2048):
+        ins = [desc((1, 4, n, 64))] * 3
+        assert plugin.get_workspace_size(ins, [desc((1, 4, n, 64))]) == 5242880
+
+
+GOOD = ((1, 4, 1000, 64), (1, 4, 777, 64), (1, 4, 777, 64), (1, 4, 1000, 64))
+
+
+def _cfg(plugin, shapes, types=(1, 1, 1, 1), fmts=(0, 0, 0, 0)):
+    ins = [dyn(s, t, f) for s, t, f in zip(shapes[:3], types[:3], fmts[:3])]
+    return plugin.configure_plugin(ins, [dyn(shapes[3], types[3], fmts[3])])
+
+
+BAD = {
+    "batch2": ((2, 4, 10, 64), (2, 4, 10, 64), (2, 4, 10, 64), (2, 4, 10, 64)),
+    "heads8": ((1, 8, 10, 64), (1, 8, 10, 64), (1, 8, 10, 64), (1, 8, 10, 64)),
+    "nq2049": ((1, 4, 2049, 64), (1, 4, 10, 64), (1, 4, 10, 64), (1, 4, 2049, 64)),
+    "nkv2049": ((1, 4, 10, 64), (1, 4, 2049, 64), (1, 4, 2049, 64), (1, 4, 10, 64)),
+    "k_ne_v": ((1, 4, 10, 64), (1, 4, 11, 64), (1, 4, 10, 64), (1, 4, 10, 64)),
+    "o_ne_q": ((1, 4, 10, 64), (1, 4, 10, 64), (1, 4, 10, 64), (1, 4, 11, 64)),
+    "d128": ((1, 4, 10, 128), (1, 4, 10, 128), (1, 4, 10, 128), (1, 4, 10, 128)),
+    "rank3": ((4, 10, 64), (1, 4, 10, 64), (1, 4, 10, 64), (1, 4, 10, 64)),
+    "nkv0": ((1, 4, 10, 64), (1, 4, 0, 64), (1, 4, 0, 64), (1, 4, 10, 64)),
+}
+
+
+def test_configure_accepts_reference_shapes(plugin):
+    _cfg(plugin, GOOD)
+    _cfg(plugin, GOOD, types=(0, 0, 0, 0))
+    _cfg(plugin, ((1, 4, 2048, 64),) * 4)
+    _cfg(plugin, ((1, 4, 1, 64),) * 4)
+
+
+@pytest.mark.parametrize("case", sorted(BAD))
+def test_configure_rejects(plugin, case):
+    from lightglue_amd import PluginError
+
+    with pytest.raises(PluginError):
+        _cfg(plugin, BAD[case])
+
+
+def test_configure_rejects_mixed_types_and_formats(plugin):
+    from lightglue_amd import PluginError
+
+    with pytest.raises(PluginError):
+        _cfg(plugin, GOOD, types=(1, 0, 1, 1))
+    with pytest.raises(PluginError):
+        _cfg(plugin, GOOD, types=(1, 1, 1, 0))
+    with pytest.raises(PluginError):
+        _cfg(plugin, GOOD, types=(2, 2, 2, 2))
+    with pytest.raises(PluginError):
+        _cfg(plugin, GOOD, fmts=(0, 0, 1, 0))
+
+
+@pytest.mark.parametrize("case", sorted(BAD))
+def test_enqueue_rejects_before_touching_the_device(plugin, case):
+    """enqueue() validates exactly like configurePlugin and returns before any launch."""
+    from lightglue_amd import PluginError
+
+    s = BAD[case]
+    with pytest.raises(PluginError):
+        plugin.enqueue([desc(x) for x in s[:3]], [desc(s[3])], [16, 32, 48], [64], 128, 0)
+
+
+def test_enqueue_rejects_null_workspace(plugin):
+    from lightglue_amd import PluginError
+
+    with pytest.raises(PluginError, match="workspace"):
+        plugin.enqueue([desc(x) for x in GOOD[:3]], [desc(GOOD[3])], [16, 32, 48], [64], 0, 0)
+
+
+def test_empty_query_is_a_noop(lib):
+    # Nq == 0: nothing to launch, success without a device.
+    assert lib.mha_hd64_launch_fp16in_fp16out(None, None, None, None, 1, 4, 0, 10, None, 0, None) == 0
+
+
+def test_launch_rejects_misaligned_and_null(lib):
+    assert lib.mha_hd64_launch_fp16in_fp16out(None, None, None, None, 1, 4, 8, 8, None, 0, None) == 1
+    assert lib.mha_hd64_launch_fp16in_fp16out(16, 16, 16, 18, 1, 4, 8, 8, None, 0, None) == 1
+    assert lib.mha_hd64_launch_fp16in_fp16out(16, 16, 16, 16, 1, 4, 8, 0, None, 0, None) == 1
+
+
+def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
+    out = (ctypes.c_int32 * 3)()
+    # metric shape 1x4x1024x1024 inside the fixed 5,242,880 B workspace
+    need = lib.mha_hd64_plan(1, 4, 1024, 1024, 5242880, out)
+    qw, splits, tps = list(out)
+    wgs = (1024 // (32 * qw)) * 4 * splits
+    assert need <= 5242880 and wgs >= 128 and splits >= 2
+    # max length still fits
+    need = lib.mha_hd64_plan(1, 4, 2048, 2048, 5242880, out)
+    assert need <= 5242880
+    # no workspace -> no split
+    lib.mha_hd64_plan(1, 4, 1024, 1024, 0, out)
+    assert out[1] == 1
+    # a big batch needs no split
+    lib.mha_hd64_plan(64, 4, 1024, 1024, 1 << 30, out)
+    assert out[1] == 1 and out[0] == 4
+
+
+def test_abort_mode_aborts_like_plugin_assert():
+    """mha_hd64_set_abort_on_error(1) reproduces PLUGIN_ASSERT's abort() (checkMacrosPlugin.cpp:118-128)."""
+    code = (
+        "import sys; sys.path.insert(0, %r);"
+        "from lightglue_amd import _lib; l=_lib.load(); l.mha_hd64_set_abort_on_error(1);"
+        "l.mha_hd64_launch_fp16in_fp16out(None,None,None,None,1,4,8,8,None,0,None)" % os.path.join(
+            REPO, "lightglue-with-flashattentionv2-tensorrt_amd"))
+    r = subprocess.run(["python", "-c", code], capture_output=True, text=True)
+    assert r.returncode != 0 and "assertion failed" in r.stderr
+
+
+def test_error_message_names_the_assertion(lib):
+    from lightglue_amd import _lib
+
+    lib.mha_hd64_launch_fp16in_fp16out(None, None, None, None, 1, 4, 8, 8, None, 0, None)
+    assert "assertion failed" in _lib.last_error()
+
+
+def test_cpu_tensors_fail_loudly():
+    import torch
+    from lightglue_amd import PluginError, mha_hd64, mha_hd64_batched
+
+    q = torch.zeros(1, 4, 8, 64, dtype=torch.float16)
+    with pytest.raises(PluginError, match="GPU"):
+        mha_hd64(q, q, q)
+    with pytest.raises(PluginError, match="GPU"):
+        mha_hd64_batched(q, q, q)
