@@ -146,6 +146,33 @@ def load_traffic(tag):
         return None
 
 
+def sweep(torch, lib, device, stream, nq, nkv):
+    """Main-kernel (+combine) time for every compiled workgroup shape and KV split, single call and
+    batched; one JSON object per line on stderr (tuning aid for plan_call)."""
+    from lightglue_amd import synth
+
+    ws_buf = torch.empty(256 << 20, dtype=torch.uint8, device=device)
+    for batch in (1, 8):
+        qn, kn, vn = synth.qkv(7, nq, nkv, batch=batch)
+        q, k, v = (torch.from_numpy(x).to(device).half().contiguous() for x in (qn, kn, vn))
+        o = torch.empty_like(q)
+        for qw, kw in ((4, 1), (2, 2), (1, 4), (4, 2), (2, 4)):
+            for splits in (1, 2, 4, 8, 16):
+                def run(mask=3):
+                    return lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), batch,
+                                                      4, nq, nkv, 0, 0, qw, kw, splits, ws_buf.data_ptr(),
+                                                      ws_buf.numel(), stream.cuda_stream, mask)
+                if run() != 0:
+                    continue
+                t_all = statistics.median(event_durations_ms(torch, run, 60, stream)[10:])
+                t_main = statistics.median(event_durations_ms(torch, lambda: run(1), 60, stream)[10:])
+                fl = call_flops(batch, 4, nq, nkv)
+                print(json.dumps({"sweep": 1, "batch": batch, "q_waves": qw, "kv_waves": kw, "splits": splits,
+                                  "main_us": round(t_main * 1e3, 2), "total_us": round(t_all * 1e3, 2),
+                                  "main_tflops": round(fl / (t_main * 1e-3) / 1e12, 1)}), file=sys.stderr,
+                      flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,6 +184,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--quick", action="store_true", help="skip the secondary measurements (profiling runs)")
+    ap.add_argument("--sweep", action="store_true", help="time every workgroup shape x KV split (stderr table)")
     args = ap.parse_args()
 
     import torch
@@ -202,9 +230,9 @@ def main():
 
     import ctypes
 
-    plan_c = (ctypes.c_int32 * 3)()
+    plan_c = (ctypes.c_int32 * 4)()
     ws_need = lib.mha_hd64_plan(1, 4, nq, nkv, 5242880, plan_c)
-    q_waves, splits, _ = list(plan_c)
+    q_waves, kv_waves, splits, _ = list(plan_c)
     flops = call_flops(1, 4, nq, nkv)
     result = {
         "metric": METRIC,
@@ -222,7 +250,8 @@ def main():
         "config": {"workload": "MHAHeadDim64 plugin enqueue, Q/K/V [1,4,1024,64] fp16 -> O fp16 "
                                "(BASELINE configs[1]); K independent calls per step-graph",
                    "batch": 1, "heads": 4, "nq": nq, "nkv": nkv, "head_dim": 64,
-                   "parallelism": f"replicas{ws}", "plan": {"q_waves": q_waves, "kv_splits": splits}},
+                   "parallelism": f"replicas{ws}",
+                   "plan": {"q_waves": q_waves, "kv_waves": kv_waves, "kv_splits": splits}},
     }
 
     if not args.quick:
@@ -231,11 +260,11 @@ def main():
 
         def main_kernel():
             lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), 1, 4, nq, nkv, 0,
-                                       0, q_waves, splits, ws_buf.data_ptr(), ws_buf.numel(), sp, 1)
+                                       0, q_waves, kv_waves, splits, ws_buf.data_ptr(), ws_buf.numel(), sp, 1)
 
         def combine_kernel():
             lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), 1, 4, nq, nkv, 0,
-                                       0, q_waves, splits, ws_buf.data_ptr(), ws_buf.numel(), sp, 2)
+                                       0, q_waves, kv_waves, splits, ws_buf.data_ptr(), ws_buf.numel(), sp, 2)
 
         def full_call():
             with torch.cuda.stream(stream):
@@ -249,7 +278,7 @@ def main():
         result["roofline"] = {
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": traffic,
-            "kernel": f"mha_hd64_fwd_kernel<f16,f16,QW={q_waves}> ({splits}-way KV split)",
+            "kernel": f"mha_hd64_fwd_kernel<f16,f16,{q_waves},{kv_waves}> ({splits}-way KV split)",
             "kernel_us": round(t_main * 1e3, 3), "combine_us": round(t_comb * 1e3, 3),
             "flops_per_launch": flops, "algorithmic_bytes_per_call": call_bytes(1, 4, nq, nkv),
         }
@@ -275,6 +304,8 @@ def main():
             "frac": round(B * flops / (tb * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
         }
 
+    if args.sweep and rank == 0:
+        sweep(torch, lib, device, stream, nq, nkv)
     if rank == 0 and not args.no_cpu_baseline and not args.quick:
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, nq, nkv)
     if rank == 0:

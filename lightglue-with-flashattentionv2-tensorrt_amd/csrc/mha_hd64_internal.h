@@ -30,19 +30,22 @@ struct Call {
 
 // Launch-shape choice for one call (exposed so tests/bench can force a variant).
 struct LaunchPlan {
-    int q_waves;          // waves per workgroup that own distinct 32-row query slices (1, 2 or 4)
+    int q_waves;          // waves per workgroup that own distinct 32-row query slices
+    int kv_waves;         // waves per workgroup that split the keys of every iteration
     int splits;           // KV split across workgroups (1 = no combine pass)
-    int tiles_per_split;  // KV super-tiles (64 * (4 / q_waves) keys) per split
+    int tiles_per_split;  // KV super-tiles (64 * kv_waves keys) per split
     size_t ws_needed;     // workspace bytes the plan uses
 };
 
-LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves = 0, int force_splits = 0);
+// Workgroup shapes compiled: (q_waves, kv_waves) in {(4,1), (2,2), (1,4), (4,2), (2,4)}.
+LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves = 0, int force_kv_waves = 0,
+                     int force_splits = 0);
 size_t split_workspace_bytes(const Call& c, int splits);
 
 // Returns hipSuccess or the launch error. phase_mask (measurement hook): bit 0 = main
 // kernel, bit 1 = split-KV combine kernel.
 hipError_t launch_attention(const Call& c, InType in, OutType out, void* workspace, size_t ws_bytes,
-                            hipStream_t stream, int force_q_waves = 0, int force_splits = 0,
-                            int phase_mask = 3);
+                            hipStream_t stream, int force_q_waves = 0, int force_kv_waves = 0,
+                            int force_splits = 0, int phase_mask = 3);
 
 }  // namespace mha_hd64

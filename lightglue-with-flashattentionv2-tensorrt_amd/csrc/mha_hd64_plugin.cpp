@@ -317,36 +317,40 @@ const char* mha_hd64_last_error(void) { return g_last_error.c_str(); }
 void mha_hd64_set_abort_on_error(int32_t enable) { g_abort_on_error = enable != 0; }
 const char* mha_hd64_build_info(void) {
     return "mha_hd64: gfx950 (CDNA4) HIP kernels, v_mfma_f32_32x32x16_f16 + ds_read_b64_tr_b16; "
-           "variants fp16->fp16, fp16->fp32, fp32->fp32; q_waves {1,2,4}; split-KV combine";
+           "variants fp16->fp16, fp16->fp32, fp32->fp32; workgroups (q,kv waves) 4x1 2x2 1x4 4x2 2x4; split-KV combine";
 }
 
 // Test/bench hook (not part of include/mha_hd64.h): launch with a forced plan
-// (q_waves/splits 0 = planner's choice); phase_mask 1 = main kernel only, 2 = combine only, 3 = both.
+// (q_waves/kv_waves/splits 0 = planner's choice); phase_mask 1 = main kernel only, 2 = combine only, 3 = both.
 int32_t mha_hd64_launch_forced(const void* q, const void* k, const void* v, void* o, int32_t batch, int32_t heads,
                                int32_t nq, int32_t nkv, int32_t in_f32, int32_t out_f32, int32_t q_waves,
-                               int32_t splits, void* workspace, size_t ws_bytes, hipStream_t stream,
-                               int32_t phase_mask) {
+                               int32_t kv_waves, int32_t splits, void* workspace, size_t ws_bytes,
+                               hipStream_t stream, int32_t phase_mask) {
     MHA_CHECK(batch >= 0 && heads >= 0 && nq >= 0 && nkv >= 0);
     if (batch == 0 || heads == 0 || nq == 0) return MHA_HD64_STATUS_SUCCESS;
     MHA_CHECK(nkv >= 1);
     const mha_hd64::Call c{q, k, v, o, batch, heads, nq, nkv};
-    const mha_hd64::LaunchPlan plan = mha_hd64::plan_call(c, workspace ? ws_bytes : 0, q_waves, splits);
+    const mha_hd64::LaunchPlan plan = mha_hd64::plan_call(c, workspace ? ws_bytes : 0, q_waves, kv_waves, splits);
+    if (q_waves != 0 && (plan.q_waves != q_waves || plan.kv_waves != kv_waves))
+        return fail(MHA_HD64_STATUS_BAD_PARAM, __FILE__, __LINE__, "forced workgroup shape is not compiled");
     if (splits > 1 && plan.splits != splits)
         return fail(MHA_HD64_STATUS_WORKSPACE, __FILE__, __LINE__, "forced split does not fit the workspace/keys");
     return launch_status(mha_hd64::launch_attention(c, in_f32 ? mha_hd64::InType::F32 : mha_hd64::InType::F16,
                                                     out_f32 ? mha_hd64::OutType::F32 : mha_hd64::OutType::F16,
-                                                    workspace, ws_bytes, stream, q_waves, splits, phase_mask),
+                                                    workspace, ws_bytes, stream, q_waves, kv_waves, splits,
+                                                    phase_mask),
                          __FILE__, __LINE__);
 }
 
-// Plan query hook for tests/bench: fills {q_waves, splits, tiles_per_split}; returns workspace bytes used.
-size_t mha_hd64_plan(int32_t batch, int32_t heads, int32_t nq, int32_t nkv, size_t ws_bytes, int32_t* out3) {
+// Plan query hook for tests/bench: fills {q_waves, kv_waves, splits, tiles_per_split}; returns workspace bytes.
+size_t mha_hd64_plan(int32_t batch, int32_t heads, int32_t nq, int32_t nkv, size_t ws_bytes, int32_t* out4) {
     const mha_hd64::Call c{nullptr, nullptr, nullptr, nullptr, batch, heads, nq, nkv};
     const mha_hd64::LaunchPlan p = mha_hd64::plan_call(c, ws_bytes);
-    if (out3) {
-        out3[0] = p.q_waves;
-        out3[1] = p.splits;
-        out3[2] = p.tiles_per_split;
+    if (out4) {
+        out4[0] = p.q_waves;
+        out4[1] = p.kv_waves;
+        out4[2] = p.splits;
+        out4[3] = p.tiles_per_split;
     }
     return p.ws_needed;
 }

@@ -111,7 +111,7 @@ SIGNATURES = {
 }
 # Test/bench hooks exported by the library but not part of the public header.
 HOOKS = {
-    "mha_hd64_launch_forced": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _S, _P, _I], _I),
+    "mha_hd64_launch_forced": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _S, _P, _I], _I),
     "mha_hd64_plan": ([_I, _I, _I, _I, _S, ctypes.POINTER(ctypes.c_int32)], _S),
 }
 

@@ -207,10 +207,10 @@ def test_launch_rejects_misaligned_and_null(lib):
 
 
 def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
-    out = (ctypes.c_int32 * 3)()
+    out = (ctypes.c_int32 * 4)()
     # metric shape 1x4x1024x1024 inside the fixed 5,242,880 B workspace
     need = lib.mha_hd64_plan(1, 4, 1024, 1024, 5242880, out)
-    qw, splits, tps = list(out)
+    qw, kw, splits, tps = list(out)
     wgs = (1024 // (32 * qw)) * 4 * splits
     assert need <= 5242880 and wgs >= 128 and splits >= 2
     # max length still fits
@@ -218,10 +218,10 @@ def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
     assert need <= 5242880
     # no workspace -> no split
     lib.mha_hd64_plan(1, 4, 1024, 1024, 0, out)
-    assert out[1] == 1
+    assert out[2] == 1
     # a big batch needs no split
     lib.mha_hd64_plan(64, 4, 1024, 1024, 1 << 30, out)
-    assert out[1] == 1 and out[0] == 4
+    assert out[2] == 1 and out[0] == 4
 
 
 def test_abort_mode_aborts_like_plugin_assert():

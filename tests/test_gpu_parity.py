@@ -79,16 +79,17 @@ def test_fp16in_fp32out_launcher(name, dev):
 
 # ---- every launch plan (query-wave split x cross-workgroup KV split) against the C oracle ----
 PLAN_SHAPES = [(1, 1), (33, 65), (100, 100), (64, 2048), (300, 129), (1024, 1024), (257, 1000)]
+WG_SHAPES = [(4, 1), (2, 2), (1, 4), (4, 2), (2, 4)]
 
 
 @pytest.mark.parametrize("nq,nkv", PLAN_SHAPES)
-@pytest.mark.parametrize("q_waves", [1, 2, 4])
+@pytest.mark.parametrize("wg", WG_SHAPES)
 @pytest.mark.parametrize("splits", [1, 2, 3, 5])
-def test_forced_plans_match_oracle(nq, nkv, q_waves, splits, dev, oracle_mod):
+def test_forced_plans_match_oracle(nq, nkv, wg, splits, dev, oracle_mod):
     from lightglue_amd import _lib, synth
 
-    kw = 4 // q_waves
-    super_total = -(-nkv // (64 * kw))
+    q_waves, kv_waves = wg
+    super_total = -(-nkv // (64 * kv_waves))
     if splits > super_total:
         pytest.skip("more splits than key tiles")
     if -(-super_total // -(-super_total // splits)) != splits:
@@ -103,7 +104,7 @@ def test_forced_plans_match_oracle(nq, nkv, q_waves, splits, dev, oracle_mod):
     for out_f32, tol in ((0, TOL), (1, TOL_F32OUT)):
         o = torch.full(q.shape, float("nan"), dtype=torch.float32 if out_f32 else torch.float16, device=dev)
         st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), 1, 4, nq, nkv, 0,
-                                        out_f32, q_waves, splits, ws.data_ptr(), ws.numel(),
+                                        out_f32, q_waves, kv_waves, splits, ws.data_ptr(), ws.numel(),
                                         torch.cuda.current_stream().cuda_stream, 3)
         assert st == 0, _lib.last_error()
         torch.cuda.synchronize()
@@ -112,8 +113,8 @@ def test_forced_plans_match_oracle(nq, nkv, q_waves, splits, dev, oracle_mod):
         assert _maxdiff(got[:, :, rows], ref) <= tol
 
 
-@pytest.mark.parametrize("q_waves", [1, 2, 4])
-def test_forced_plans_f32_input(q_waves, dev, oracle_mod):
+@pytest.mark.parametrize("wg", WG_SHAPES)
+def test_forced_plans_f32_input(wg, dev, oracle_mod):
     from lightglue_amd import _lib, synth
 
     lib = _lib.load()
@@ -124,10 +125,48 @@ def test_forced_plans_f32_input(q_waves, dev, oracle_mod):
     o = torch.empty_like(q)
     ws = torch.empty(16 << 20, dtype=torch.uint8, device=dev)
     st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), 1, 4, nq, nkv, 1, 1,
-                                    q_waves, 2, ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream, 3)
+                                    wg[0], wg[1], 2, ws.data_ptr(), ws.numel(),
+                                    torch.cuda.current_stream().cuda_stream, 3)
     assert st == 0, _lib.last_error()
     torch.cuda.synchronize()
     assert _maxdiff(o.cpu().numpy(), ref) <= TOL
+
+
+def test_rescale_branch_forced(dev, oracle_mod):
+    """Rule 26 (cdna_hip_programming.md §5.4): force the lazy-rescale branch at a chosen tile.
+
+    Query row 5 meets a key row (600) scaled so its score jumps far past the running max
+    of the first tiles; every other query keeps its max. Checked on the full tensor."""
+    from lightglue_amd import mha_hd64, synth
+
+    nq, nkv = 256, 1024
+    qn, kn, vn = synth.qkv(606, nq, nkv)
+    for gain in (0.5, 2.0, 6.0):
+        k2 = synth.spike(qn, kn, 5, 600, gain)
+        q16, k16, v16 = (synth.round_f16(x) for x in (qn, k2, vn))
+        ref = oracle_mod.attention_c(q16, k16, v16)
+        q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+        o = mha_hd64(q, k, v)
+        torch.cuda.synchronize()
+        assert _maxdiff(o.float().cpu().numpy(), ref) <= TOL, gain
+
+
+def test_large_negative_logits(dev, oracle_mod):
+    """Scores far below zero everywhere: the first tile must set the max exactly (no underflow to l = 0)."""
+    from lightglue_amd import mha_hd64, synth
+
+    nq, nkv = 64, 300
+    qn, kn, vn = synth.qkv(808, nq, nkv)
+    qn = np.abs(qn) * 4
+    kn = -np.abs(kn) * 4  # every score strongly negative (~ -200 raw)
+    q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
+    ref = oracle_mod.attention_c(q16, k16, v16)
+    q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+    o = mha_hd64(q, k, v)
+    torch.cuda.synchronize()
+    got = o.float().cpu().numpy()
+    assert np.isfinite(got).all()
+    assert _maxdiff(got, ref) <= TOL
 
 
 def test_batched_launcher_many_pairs(dev, oracle_mod):
