@@ -156,7 +156,7 @@ def sweep(torch, lib, device, stream, nq, nkv):
         qn, kn, vn = synth.qkv(7, nq, nkv, batch=batch)
         q, k, v = (torch.from_numpy(x).to(device).half().contiguous() for x in (qn, kn, vn))
         o = torch.empty_like(q)
-        for qw, kw in ((4, 1), (2, 2), (1, 4), (4, 2), (2, 4)):
+        for qw, kw in ((4, 1), (2, 2), (1, 2), (4, 2)):
             for splits in (1, 2, 4, 8, 16):
                 def run(mask=3):
                     return lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), batch,
@@ -173,6 +173,22 @@ def sweep(torch, lib, device, stream, nq, nkv):
                       flush=True)
 
 
+def profile_driver(torch, args, device):
+    """Eager launches of one workload (for rocprofv3 --kernel-trace / --pmc passes)."""
+    import lightglue_amd
+    from lightglue_amd import synth
+
+    B = 1 if args.only == "call" else args.batched
+    qn, kn, vn = synth.qkv(11, args.nq, args.nkv, batch=B)
+    q, k, v = (torch.from_numpy(x).to(device).half().contiguous() for x in (qn, kn, vn))
+    o = torch.empty_like(q)
+    fn = (lambda: lightglue_amd.mha_hd64(q, k, v, out=o)) if B == 1 else (
+        lambda: lightglue_amd.mha_hd64_batched(q, k, v, out=o))
+    for _ in range(args.warmup + args.steps):
+        fn()
+    torch.cuda.synchronize()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -185,6 +201,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--quick", action="store_true", help="skip the secondary measurements (profiling runs)")
     ap.add_argument("--sweep", action="store_true", help="time every workgroup shape x KV split (stderr table)")
+    ap.add_argument("--only", choices=["call", "batched"], default=None,
+                    help="profiling driver: launch just this workload --steps times (eager), print nothing else")
     args = ap.parse_args()
 
     import torch
@@ -204,6 +222,9 @@ def main():
 
     lib = _lib.load()
     nq, nkv = args.nq, args.nkv
+    if args.only:
+        profile_driver(torch, args, device)
+        return
     qn, kn, vn = synth.qkv(100 + rank, nq, nkv)
     q, k, v = (torch.from_numpy(x).to(device).half().contiguous() for x in (qn, kn, vn))
     out = torch.empty_like(q)

@@ -37,7 +37,7 @@ struct LaunchPlan {
     size_t ws_needed;     // workspace bytes the plan uses
 };
 
-// Workgroup shapes compiled: (q_waves, kv_waves) in {(4,1), (2,2), (1,4), (4,2), (2,4)}.
+// Workgroup shapes compiled: (q_waves, kv_waves) in {(4,1), (2,2), (1,2), (4,2)}.
 LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves = 0, int force_kv_waves = 0,
                      int force_splits = 0);
 size_t split_workspace_bytes(const Call& c, int splits);
@@ -47,5 +47,8 @@ size_t split_workspace_bytes(const Call& c, int splits);
 hipError_t launch_attention(const Call& c, InType in, OutType out, void* workspace, size_t ws_bytes,
                             hipStream_t stream, int force_q_waves = 0, int force_kv_waves = 0,
                             int force_splits = 0, int phase_mask = 3);
+
+// Diagnostic builds (-DMHA_STAMPS): where the kernel writes its per-workgroup timestamps.
+void set_stamp_buffer(void* p);
 
 }  // namespace mha_hd64

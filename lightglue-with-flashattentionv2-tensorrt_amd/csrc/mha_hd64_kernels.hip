@@ -37,6 +37,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "mha_hd64_internal.h"
 
@@ -67,6 +68,9 @@ struct FwdArgs {
     int nkv;
     int splits;
     int tiles_per_split;
+    int qtiles;      // query blocks per (batch, head)
+    int bh;          // batch * heads
+    unsigned long long* stamps;  // diagnostic builds only (MHA_STAMPS): 8 x u64 per workgroup
 };
 
 // LDS images (byte offsets inside one 8 KiB [64 rows][128 B] tile; chunk = 16 B = 8 halfs).
@@ -131,9 +135,20 @@ __device__ __forceinline__ float tree_sum(const f32x16& a, const f32x16& b) {
     return t[0];
 }
 
-__device__ __forceinline__ f16x4 tr_read(const char* lds_base, int byte_off) {
-    const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(lds_base + byte_off));
+// LDS accesses through an explicit address-space-3 base and 32-bit byte offsets, so the
+// compiler folds the compile-time part of every address into the DS instruction's offset field.
+typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((address_space(3))) f16x8 lds_f16x8;
+
+__device__ __forceinline__ f16x4 tr_read(lds_char* lds, unsigned byte_off) {
+    const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(lds + byte_off));
     return __builtin_bit_cast(f16x4, v);
+}
+__device__ __forceinline__ f16x8 lds_read16(lds_char* lds, unsigned byte_off) {
+    return *(lds_f16x8*)(lds + byte_off);
+}
+__device__ __forceinline__ void lds_write16(lds_char* lds, unsigned byte_off, f16x8 v) {
+    *(lds_f16x8*)(lds + byte_off) = v;
 }
 
 __device__ __forceinline__ f16x8 cat8(f16x4 a, f16x4 b) {
@@ -155,8 +170,64 @@ __device__ __forceinline__ f32x16 splat16(float x) {
     return f32x16{x, x, x, x, x, x, x, x, x, x, x, x, x, x, x, x};
 }
 
+// Diagnostic ablation switches (tools/ablate_build.sh builds each into lib/exp/; the shipped
+// library defines none of them). Results of an ablated build are wrong by construction.
+#ifndef MHA_ABL
+#define MHA_ABL 0
+#endif
+#define ABL_NO_BARRIER 1
+#define ABL_NO_REFILL 2
+#define ABL_NO_EXP 4
+#define ABL_NO_SOFTMAX 8
+#define ABL_NO_PV 16
+#define ABL_NO_QK 32
+#define ABL_QK_NO_LDS_DEP 64
+__device__ __forceinline__ void keep_live(const f16x8& x) { asm volatile("" ::"v"(x)); }
+
+// In-kernel timestamps (diagnostic build -DMHA_STAMPS only): s_memtime after draining memory.
+#ifdef MHA_STAMPS
+#define STAMP(slot)                                                                                       \
+    do {                                                                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                                                \
+        unsigned long long t_;                                                                            \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                                                \
+        if (threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (slot)] = t_;                                     \
+    } while (0)
+#else
+#define STAMP(slot) \
+    do {            \
+    } while (0)
+#endif
+
+constexpr float kMaskBias = -65504.f;  // fp16 lowest: a masked key's score, exp2 -> 0
+constexpr float kEmptyMax = -30000.f;  // tile max below this: every key of the tile was masked
+
+// Buffer loads (T8): a per-head descriptor whose record count is the head's byte size, so
+// rows past nq / nkv read as zeros in hardware (no clamps, no 64-bit address math per load);
+// the per-iteration key offset rides in the scalar soffset.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ void bload8(Raw8<f16>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff) {
+    r.x = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+__device__ __forceinline__ void bload8(Raw8<float>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff) {
+    r.a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+    r.b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16, soff, 0));
+}
+
 // ----------------------------------------------------------------------------------------
 // Main kernel. Grid: x = query blocks of 32*QW rows, y = batch*heads, z = KV splits.
+//
+// Software pipeline per wave (tile t = this wave's 64 keys of super-tile t):
+//   phase A:  QKᵀ MFMAs of tile t+1            ‖ exp / row-sum / f16-pack of tile t (VALU)
+//   phase B:  PV MFMAs of tile t               ‖ tail mask + row max of tile t+1 (VALU)
+// so the matrix pipe and the vector pipe of a SIMD work on independent data. LDS is a
+// 3-stage ring of super-tiles: iteration t reads V(t) and K(t+1) and fills stage t+2
+// (loaded into registers at the start of the iteration, written after phase B), one
+// barrier per iteration.
 // ----------------------------------------------------------------------------------------
 template <typename TIn, typename TOut, int QW, int KW>
 __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a) {
@@ -164,10 +235,15 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     constexpr int BLOCK_M = 32 * QW;                // query rows per workgroup
     constexpr int SUPER = kTileKV * KW;             // keys per iteration
     constexpr int STAGE_BYTES = KW * 2 * kTileBytes;
+    constexpr int NSTAGE = 3;
     constexpr int NLOAD = (2 * KW * 512) / NT;      // 16-B chunks staged per thread per iteration
+    constexpr unsigned SZ = sizeof(TIn);
     static_assert(NLOAD * NT == 2 * KW * 512, "staging must divide evenly");
-    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+    static_assert(NSTAGE * STAGE_BYTES <= 160 * 1024, "LDS ring exceeds 160 KiB");
+    __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE_BYTES];
+    lds_char* const lds = (lds_char*)smem;
 
+    STAMP(0);
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
@@ -176,229 +252,336 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     const int qw = wave % QW;
     const int kw = wave / QW;
     const int nq = a.nq, nkv = a.nkv;
-    const int bh = blockIdx.y;
-    const int split = blockIdx.z;
+    // XCD-aware order (T1): the dispatcher deals consecutive blocks round-robin over the 8 XCDs;
+    // renumber so that the blocks sharing one XCD are consecutive query blocks of the same
+    // (batch, head, split), i.e. read the same K/V through the same L2. Bijective for any count.
+    int qtile, bh, split;
+    {
+        const int T = gridDim.x, L = blockIdx.x;
+        const int q8 = T >> 3, r8 = T & 7, xcd = L & 7;
+        const int j = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+        qtile = j % a.qtiles;
+        const int rest = j / a.qtiles;
+        bh = rest % a.bh;
+        split = rest / a.bh;
+    }
 
     const TIn* Qb = reinterpret_cast<const TIn*>(a.q) + (size_t)bh * nq * kHeadDim;
     const TIn* Kb = reinterpret_cast<const TIn*>(a.k) + (size_t)bh * nkv * kHeadDim;
     const TIn* Vb = reinterpret_cast<const TIn*>(a.v) + (size_t)bh * nkv * kHeadDim;
-    const int q_row = blockIdx.x * BLOCK_M + qw * 32 + r;
+    const __amdgpu_buffer_rsrc_t q_rs = make_rsrc(Qb, (unsigned)nq * kHeadDim * SZ);
+    const __amdgpu_buffer_rsrc_t k_rs = make_rsrc(Kb, (unsigned)nkv * kHeadDim * SZ);
+    const __amdgpu_buffer_rsrc_t v_rs = make_rsrc(Vb, (unsigned)nkv * kHeadDim * SZ);
+    const int q_row = qtile * BLOCK_M + qw * 32 + r;
 
     const int super_total = (nkv + SUPER - 1) / SUPER;
     const int st_begin = split * a.tiles_per_split;
     const int st_end = min(super_total, st_begin + a.tiles_per_split);
     const int n_iter = max(0, st_end - st_begin);
 
-    // Staging: chunk i of this thread -> (tile, K|V) = id / 512, row = (id % 512) / 8, chunk = id % 8.
-    Raw8<TIn> stg[NLOAD];
-    auto issue = [&](int it) {
-        const int kv_base = (st_begin + it) * SUPER;
+    // Staging: load i of this thread covers tile-tensor tt = i / PER (tile tt/2, K or V by tt&1),
+    // row (i % PER) * (NT/8) + tid/8, 16-B chunk tid%8. tt is compile-time, so the K/V descriptor
+    // choice stays scalar (no waterfall loop around the buffer load).
+    constexpr int PER = 512 / NT;  // loads per thread per 8 KiB tile-tensor
+    static_assert(PER * NT == 512, "workgroup size must divide a tile");
+    // Two staging register sets: the loads of super-tile t+3 are issued at step t (two steps
+    // of latency cover for first-touch MALL/HBM reads) while set t+2 is written to LDS.
+    Raw8<TIn> stgA[NLOAD], stgB[NLOAD];
+    auto issue = [&](int it, Raw8<TIn>(&stg)[NLOAD]) {
+        const unsigned soff = (unsigned)(st_begin + it) * SUPER * kHeadDim * SZ;
 #pragma unroll
         for (int i = 0; i < NLOAD; ++i) {
-            const int id = i * NT + tid;
-            const int tt = id >> 9;
-            const int row = (id & 511) >> 3;
-            const int g = min(kv_base + (tt >> 1) * kTileKV + row, nkv - 1);  // clamp: masked keys read a valid row
-            load8(stg[i], ((tt & 1) ? Vb : Kb) + (size_t)g * kHeadDim + (tid & 7) * 8);
+            const int tt = i / PER;
+            const int row = (i % PER) * (NT / 8) + (tid >> 3);
+            const unsigned voff = (unsigned)(((tt >> 1) * kTileKV + row) * kHeadDim + (tid & 7) * 8) * SZ;
+            bload8(stg[i], (tt & 1) ? v_rs : k_rs, voff, soff);
         }
     };
-    auto write = [&](int stage) {
+    auto write = [&](int stage, const Raw8<TIn>(&stg)[NLOAD]) {
 #pragma unroll
         for (int i = 0; i < NLOAD; ++i) {
-            const int id = i * NT + tid;
-            const int tt = id >> 9;
-            const int row = (id & 511) >> 3;
+            const int tt = i / PER;
+            const int row = (i % PER) * (NT / 8) + (tid >> 3);
             const int ch = tid & 7;
-            char* dst = smem + stage * STAGE_BYTES + tt * kTileBytes + ((tt & 1) ? v_off(row, ch) : k_off(row, ch));
-            *reinterpret_cast<f16x8*>(dst) = to_f16(stg[i]);
+            lds_write16(lds, stage * STAGE_BYTES + tt * kTileBytes + ((tt & 1) ? v_off(row, ch) : k_off(row, ch)),
+                        to_f16(stg[i]));
         }
     };
-
-    if (n_iter > 0) issue(0);
 
     // Q fragments (B operand of Sᵀ = K·Qᵀ): lane holds Q[q_row][16s + 8hh .. +7] * 0.125*log2(e), fp16.
     f16x8 qf[4];
-    {
-        const int qr = min(q_row, nq - 1);  // rows past nq are computed on a valid row and never stored
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            Raw8<TIn> t;
-            load8(t, Qb + (size_t)qr * kHeadDim + 16 * s + 8 * hh);
-            const f16x8 h = to_f16(t);
+    for (int s = 0; s < 4; ++s) {
+        Raw8<TIn> t;
+        bload8(t, q_rs, (unsigned)(q_row * kHeadDim + 16 * s + 8 * hh) * SZ, 0);
+        const f16x8 h = to_f16(t);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) qf[s][e] = (f16)((float)h[e] * kScaleLog2);
-        }
+        for (int e = 0; e < 8; ++e) qf[s][e] = (f16)((float)h[e] * kScaleLog2);
     }
 
-    if (n_iter > 0) write(0);
+    // Prologue: stages 0 and 1 (super-tiles 0 and 1); super-tile 2 in flight in set A.
+    if (n_iter > 0) issue(0, stgA);
+    if (n_iter > 1) issue(1, stgB);
+    if (n_iter > 0) write(0, stgA);
+    if (n_iter > 1) write(1, stgB);
+    if (n_iter > 2) issue(2, stgA);
     __syncthreads();
+    STAMP(1);
 
     // Per-lane LDS addressing (compile-time parts are added as immediates).
-    int k_addr[4];
+    unsigned k_addr[4];  // + (kw * 2) * kTileBytes: this wave's K tile inside a stage
 #pragma unroll
-    for (int s = 0; s < 4; ++s) k_addr[s] = k_off(r, 2 * s + hh);
+    for (int s = 0; s < 4; ++s) k_addr[s] = k_off(r, 2 * s + hh) + (kw * 2) * kTileBytes;
     // V tr-read: lane (group g, idx 4qq+pp) supplies row (4hh + qq) + const, columns
     // 32dt + 16(g&1) + 4pp. Swizzle bit b = (qq>>1)&1 flips the 64-B half (dt).
     const int g16 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
     const int vb = (qq >> 1) & 1;
     const int v_lane = 128 * (4 * hh + qq) + 16 * (2 * (g16 & 1) + (pp >> 1)) + 8 * (pp & 1);
-    const int v_addr0 = v_lane + 64 * vb;        // dims 0..31
-    const int v_addr1 = v_lane + 64 * (1 - vb);  // dims 32..63
+    const unsigned v_addr0 = v_lane + 64 * vb + (kw * 2 + 1) * kTileBytes;        // dims 0..31
+    const unsigned v_addr1 = v_lane + 64 * (1 - vb) + (kw * 2 + 1) * kTileBytes;  // dims 32..63
 
     float m_run = 0.f;        // reference max of this lane's query, log2 units (s·c)
     float l_run = 0.f;        // running sum, in-lane partial (the two halves hold disjoint keys)
-    f32x16 cinit = {};        // = -m_run in every element: C operand of the first QK MFMA
+    // Bias k-step of the QKᵀ chains: A (key side) = [1, 1, mask] per key row, B (query side) =
+    // [-m_hi, -m_lo, 1] per query, in k-slots 0..2 of the lower half-wave (zeros elsewhere).
+    // One extra MFMA per chain adds -m (fp16 hi + lo, error ~|m|·2^-22) and the tail mask, so
+    // the chain starts from an inline-zero C (no register copy) and the softmax needs no
+    // subtraction and no masking VALU.
+    const f16 one_h = hh == 0 ? (f16)1.f : (f16)0.f;
+    const f16x8 a_bias = f16x8{one_h, one_h, 0, 0, 0, 0, 0, 0};
+    f16x8 b_bias = f16x8{0, 0, one_h, 0, 0, 0, 0, 0};  // m_run = 0
+    auto set_bias = [&]() {
+        const f16 hi = (f16)(-m_run);
+        const f16 lo = (f16)(-m_run - (float)hi);
+        b_bias = hh == 0 ? f16x8{hi, lo, (f16)1.f, 0, 0, 0, 0, 0} : f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    };
     f32x16 o0 = {}, o1 = {};  // Oᵀ tiles: dims 0..31 and 32..63, query on the lane
 
-    for (int it = 0; it < n_iter; ++it) {
-        if (it + 1 < n_iter) issue(it + 1);
-        const int cur = it & 1;
-        const char* Kt = smem + cur * STAGE_BYTES + (kw * 2) * kTileBytes;
-        const char* Vt = Kt + kTileBytes;
-        const int kv0 = (st_begin + it) * SUPER + kw * kTileKV;
-
-        // ---- Sᵀ = K·Qᵀ·c - m for keys kv0..kv0+31 (s0) and kv0+32..kv0+63 (s1) ----
+    // QKᵀ of super-tile t (this wave's tile), scores relative to m_run.
+    // QKᵀ of the tile in stage kstage: scores s·c - m (log2 units), masked keys at ~-65504.
+    auto qk = [&](unsigned kstage, const f16x8& ab0, const f16x8& ab1, f32x16& s0, f32x16& s1) {
         f16x8 kf[8];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            kf[2 * s] = *reinterpret_cast<const f16x8*>(Kt + k_addr[s]);
-            kf[2 * s + 1] = *reinterpret_cast<const f16x8*>(Kt + k_addr[s] + 32 * 128);
+            const unsigned ka = k_addr[s] + kstage;
+            kf[2 * s] = lds_read16(lds, ka);
+            kf[2 * s + 1] = lds_read16(lds, ka + 32 * 128);
         }
-        f32x16 s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[0], qf[0], cinit, 0, 0, 0);
-        f32x16 s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[1], qf[0], cinit, 0, 0, 0);
+        const f32x16 zero = {};
+        if (MHA_ABL & ABL_NO_QK) {
 #pragma unroll
-        for (int s = 1; s < 4; ++s) {
+            for (int s = 0; s < 8; ++s) keep_live(kf[s]);
+            s0 = zero;
+            s1 = zero;
+            return;
+        }
+        s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab0, b_bias, zero, 0, 0, 0);
+        s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab1, b_bias, zero, 0, 0, 0);
+        if (MHA_ABL & ABL_QK_NO_LDS_DEP) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(qf[(s + 1) & 3], qf[s], s0, 0, 0, 0);
+                s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(qf[(s + 2) & 3], qf[s], s1, 0, 0, 0);
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s) keep_live(kf[s]);
+            return;
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
             s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s], qf[s], s0, 0, 0, 0);
             s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s + 1], qf[s], s1, 0, 0, 0);
         }
+    };
+    // Tail mask (reference: last KV tile only, …fp16out.cu:475-494): the bias A operand of the
+    // tile carries kMaskBias in k-slot 2 for key rows >= nkv. Only the last super-tile of the
+    // call can hold such keys; the steady-state loop below never runs it.
+    auto a_bias_tile = [&](int t, int half) -> f16x8 {
+        const int key = (st_begin + t) * SUPER + kw * kTileKV + 32 * half + r;
+        const f16 mk = (hh == 0 && key >= nkv) ? (f16)kMaskBias : (f16)0.f;
+        return f16x8{one_h, one_h, mk, 0, 0, 0, 0, 0};
+    };
+    const bool tail = (st_begin + n_iter) * SUPER > nkv;  // last super-tile of this split is partial
 
-        // ---- tail mask (reference: last KV tile only, …fp16out.cu:475-494); wave-uniform ----
-        if (kv0 + kTileKV > nkv) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int kk = kv0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-                if (kk >= nkv) s0[i] = -INFINITY;
-                if (kk + 32 >= nkv) s1[i] = -INFINITY;
-            }
-        }
+    // Ring stage of tile `it` (scalar, advanced once per step: no modulo per access).
+    int st_cur = 0;
+    auto next_stage = [](int st) { return st == NSTAGE - 1 ? 0 : st + 1; };
+    // Step `it` writes super-tile it+2 from set `wr` and issues super-tile it+3 into set `is`.
+    auto step = [&](int it, f32x16& c0, f32x16& c1, float mxc, f32x16& n0, f32x16& n1, float& mxn,
+                    auto has_next_c, bool mask_next, Raw8<TIn>(&wr)[NLOAD], Raw8<TIn>(&is)[NLOAD]) {
+        constexpr bool HAS_NEXT = decltype(has_next_c)::value;
+        const int st_nxt = next_stage(st_cur);
+        const int st_fill = next_stage(st_nxt);
+        if (!(MHA_ABL & ABL_NO_REFILL) && it + 3 < n_iter) issue(it + 3, is);
 
-        // ---- online softmax (per lane = per query), scores already relative to m_run ----
-        // First tile: set the max exactly. Later tiles: move it only when some query's tile
-        // max exceeds it by more than kRescaleThr (wave-uniform, rare).
-        const float mx = xhalf_max(tree_max(s0, s1));
+        // online-softmax decision for tile `it` (first tile: set the max exactly; later tiles:
+        // move it only when some query's tile max exceeds it by > kRescaleThr)
         const bool first = (it == 0);
-        if (first || __builtin_amdgcn_ballot_w64(mx > kRescaleThr) != 0) {
-            const float d = first ? ((mx == -INFINITY) ? 0.f : mx)  // a fully masked tile keeps m = 0
-                                  : fmaxf(mx, 0.f);
+        if (first || __builtin_amdgcn_ballot_w64(mxc > kRescaleThr) != 0) {  // wave-uniform, rare
+            const float d = first ? ((mxc < kEmptyMax) ? 0.f : mxc)  // a fully masked tile keeps m = 0
+                                  : fmaxf(mxc, 0.f);
             const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-d);
             o0 *= alpha;
             o1 *= alpha;
             l_run *= alpha;
             m_run += d;
-            s0 -= d;
-            s1 -= d;
-            cinit = splat16(-m_run);
+            c0 -= d;
+            c1 -= d;
+            set_bias();
         }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            s0[i] = __builtin_amdgcn_exp2f(s0[i]);
-            s1[i] = __builtin_amdgcn_exp2f(s1[i]);
-        }
-        l_run += tree_sum(s0, s1);
 
-        // ---- P (f16) as the B operand: registers 8ss..8ss+7 of a 32x32 tile = k-step ss ----
-        f16x8 p[2][2];
+        // phase A: QKᵀ(it+1) on the matrix pipe ‖ softmax(it) on the vector pipe
+        if constexpr (HAS_NEXT) {
+            if (mask_next)
+                qk((unsigned)st_nxt * STAGE_BYTES, a_bias_tile(it + 1, 0), a_bias_tile(it + 1, 1), n0, n1);
+            else
+                qk((unsigned)st_nxt * STAGE_BYTES, a_bias, a_bias, n0, n1);
+        }
+        if (!(MHA_ABL & (ABL_NO_EXP | ABL_NO_SOFTMAX))) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                c0[i] = __builtin_amdgcn_exp2f(c0[i]);
+                c1[i] = __builtin_amdgcn_exp2f(c1[i]);
+            }
+        }
+        if (!(MHA_ABL & ABL_NO_SOFTMAX)) l_run += tree_sum(c0, c1);
+        f16x8 p[2][2];  // P (f16) as the B operand: registers 8ss..8ss+7 of a 32x32 tile = k-step ss
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-            p[0][0][e] = (f16)s0[e];
-            p[0][1][e] = (f16)s0[8 + e];
-            p[1][0][e] = (f16)s1[e];
-            p[1][1][e] = (f16)s1[8 + e];
+            p[0][0][e] = (f16)c0[e];
+            p[0][1][e] = (f16)c0[8 + e];
+            p[1][0][e] = (f16)c1[e];
+            p[1][1][e] = (f16)c1[8 + e];
         }
 
-        // ---- Oᵀ += Vᵀ·Pᵀ, Vᵀ fragments by transposing LDS reads ----
+        // phase B: Oᵀ += Vᵀ·Pᵀ (it) on the matrix pipe ‖ row max (it+1)
+        const unsigned va0 = v_addr0 + (unsigned)st_cur * STAGE_BYTES;
+        const unsigned va1 = v_addr1 + (unsigned)st_cur * STAGE_BYTES;
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
-                const int rowc = 128 * (32 * j + 16 * ss);
-                const f16x8 va = cat8(tr_read(Vt, v_addr0 + rowc), tr_read(Vt, v_addr0 + rowc + 8 * 128));
-                const f16x8 vb8 = cat8(tr_read(Vt, v_addr1 + rowc), tr_read(Vt, v_addr1 + rowc + 8 * 128));
-                o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, p[j][ss], o0, 0, 0, 0);
-                o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vb8, p[j][ss], o1, 0, 0, 0);
-            }
-
-        if (it + 1 < n_iter) write((it + 1) & 1);
-        __syncthreads();
-    }
-
-    // A wave that saw no key (all of its tiles past nkv) must not set the merged max.
-    float m_eff = (l_run > 0.f) ? m_run : -INFINITY;
-
-    // ---- merge the KW key-split waves of this workgroup through LDS ----
-    if constexpr (KW > 1) {
-        float* red_m = reinterpret_cast<float*>(smem);  // [KW][QW][64]
-        float* red_o = red_m + KW * QW * 64;            // [KW-1][QW][33][64]
-        red_m[(kw * QW + qw) * 64 + lane] = m_eff;
-        __syncthreads();
-        float M = -INFINITY;
-#pragma unroll
-        for (int k = 0; k < KW; ++k) M = fmaxf(M, red_m[(k * QW + qw) * 64 + lane]);
-        const float w = (m_eff == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_eff - M);
-        o0 *= w;
-        o1 *= w;
-        l_run *= w;
-        if (kw > 0) {
-            float* dst = red_o + ((kw - 1) * QW + qw) * 33 * 64 + lane;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                dst[i * 64] = o0[i];
-                dst[(16 + i) * 64] = o1[i];
-            }
-            dst[32 * 64] = l_run;
-        }
-        __syncthreads();
-        if (kw == 0) {
-#pragma unroll
-            for (int k = 1; k < KW; ++k) {
-                const float* src = red_o + ((k - 1) * QW + qw) * 33 * 64 + lane;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    o0[i] += src[i * 64];
-                    o1[i] += src[(16 + i) * 64];
+                const unsigned rowc = 128 * (32 * j + 16 * ss);
+                const f16x8 va = cat8(tr_read(lds, va0 + rowc), tr_read(lds, va0 + rowc + 8 * 128));
+                const f16x8 vb8 = cat8(tr_read(lds, va1 + rowc), tr_read(lds, va1 + rowc + 8 * 128));
+                if (MHA_ABL & ABL_NO_PV) {
+                    keep_live(va);
+                    keep_live(vb8);
+                    keep_live(p[j][ss]);
+                } else {
+                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, p[j][ss], o0, 0, 0, 0);
+                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vb8, p[j][ss], o1, 0, 0, 0);
                 }
-                l_run += src[32 * 64];
+            }
+        if constexpr (HAS_NEXT) {
+            if (MHA_ABL & ABL_NO_SOFTMAX) mxn = 0.f;
+            else mxn = xhalf_max(tree_max(n0, n1));
+        }
+
+        if (!(MHA_ABL & ABL_NO_REFILL) && it + 2 < n_iter) write(st_fill, wr);
+        if (!(MHA_ABL & ABL_NO_BARRIER)) __syncthreads();
+        st_cur = st_nxt;
+    };
+
+    // Scores ping-pong between two named register sets (no runtime-indexed arrays, no copies).
+    f32x16 sA0, sA1, sB0, sB1;
+    float mxA = 0.f, mxB = 0.f;
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    if (n_iter > 0) {
+        if (tail && n_iter == 1)
+            qk(0u, a_bias_tile(0, 0), a_bias_tile(0, 1), sA0, sA1);
+        else
+            qk(0u, a_bias, a_bias, sA0, sA1);
+        mxA = xhalf_max(tree_max(sA0, sA1));
+    }
+    int it = 0;
+    // Steady state: tiles it+1 and it+2 exist and neither is the (possibly partial) last one.
+    for (; it + 3 < n_iter; it += 2) {
+        step(it, sA0, sA1, mxA, sB0, sB1, mxB, T_{}, false, stgA, stgB);
+        step(it + 1, sB0, sB1, mxB, sA0, sA1, mxA, T_{}, false, stgB, stgA);
+    }
+    // Tail (at most 3 iterations): same step with the mask flag live; scores and the pending
+    // staging set move back to A after each step.
+    for (; it + 1 < n_iter; ++it) {
+        step(it, sA0, sA1, mxA, sB0, sB1, mxB, T_{}, tail && (it + 2 == n_iter), stgA, stgB);
+        sA0 = sB0;
+        sA1 = sB1;
+        mxA = mxB;
+#pragma unroll
+        for (int i = 0; i < NLOAD; ++i) stgA[i] = stgB[i];
+    }
+    if (it < n_iter) step(it, sA0, sA1, mxA, sB0, sB1, mxB, F_{}, false, stgA, stgB);
+    STAMP(2);
+
+    // ---- epilogue ----
+    // Every wave stages its Oᵀ accumulators as fp32 rows (at its own max) plus (m, l) in LDS;
+    // then all threads merge the KW key-split partials of a row and write whole 16-byte row
+    // chunks (a wave stores complete rows: coalesced, few store instructions).
+    // A wave that saw no key (all of its tiles past nkv) gets m = -inf (weight 0). The test uses
+    // the cross-half total: the halves hold disjoint keys but the SAME query's m and O dims.
+    const float L_w = xhalf_sum(l_run);
+    const float m_w = (L_w > 0.f) ? m_run : -INFINITY;
+    constexpr int OROW = 68;  // fp32 row pitch in LDS: 64 dims + 4 pad (rows r, r+1 on different banks)
+    float* ol = reinterpret_cast<float*>(smem);     // [KW][BLOCK_M][OROW]
+    float* mlb = ol + KW * BLOCK_M * OROW;          // [KW][BLOCK_M][2]
+    static_assert((KW * BLOCK_M * OROW + KW * BLOCK_M * 2) * 4 <= NSTAGE * STAGE_BYTES, "epilogue LDS");
+    {
+        const int row = qw * 32 + r;
+        float* dst = ol + (kw * BLOCK_M + row) * OROW;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int d = 8 * g4 + 4 * hh;
+            *reinterpret_cast<f32x4*>(dst + d) = f32x4{o0[4 * g4], o0[4 * g4 + 1], o0[4 * g4 + 2], o0[4 * g4 + 3]};
+            *reinterpret_cast<f32x4*>(dst + 32 + d) =
+                f32x4{o1[4 * g4], o1[4 * g4 + 1], o1[4 * g4 + 2], o1[4 * g4 + 3]};
+        }
+        if (hh == 0) *reinterpret_cast<float2*>(mlb + (kw * BLOCK_M + row) * 2) = make_float2(m_w, L_w);
+    }
+    __syncthreads();
+    STAMP(3);
+
+    // Thread -> (row, chunk of 8 dims); 8 threads per row, NT/8 rows per pass.
+    const int q_base = qtile * BLOCK_M;
+#pragma unroll
+    for (int pass = 0; pass < (BLOCK_M * 8) / NT; ++pass) {
+        const int idx = pass * NT + tid;
+        const int row = idx >> 3;
+        const int c8 = (idx & 7) * 8;
+        const int q = q_base + row;
+        float M = -INFINITY;
+        float2 ml[KW];
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            ml[k] = *reinterpret_cast<const float2*>(mlb + (k * BLOCK_M + row) * 2);
+            M = fmaxf(M, ml[k].x);
+        }
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        float L = 0.f;
+#pragma unroll
+        for (int k = 0; k < KW; ++k) {
+            const float w = (ml[k].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[k].x - M);
+            L += w * ml[k].y;
+            const float* src = ol + (k * BLOCK_M + row) * OROW + c8;
+            acc0 += w * *reinterpret_cast<const f32x4*>(src);
+            acc1 += w * *reinterpret_cast<const f32x4*>(src + 4);
+        }
+        if (q < nq) {
+            if (a.splits == 1) {
+                const float inv = 1.f / L;
+                TOut* dst = reinterpret_cast<TOut*>(a.o) + ((size_t)bh * nq + q) * kHeadDim + c8;
+                store4<TOut>(dst, acc0[0] * inv, acc0[1] * inv, acc0[2] * inv, acc0[3] * inv);
+                store4<TOut>(dst + 4, acc1[0] * inv, acc1[1] * inv, acc1[2] * inv, acc1[3] * inv);
+            } else {
+                const size_t prow = ((size_t)bh * a.splits + split) * nq + q;
+                float* dst = a.part_o + prow * kHeadDim + c8;
+                *reinterpret_cast<f32x4*>(dst) = acc0;
+                *reinterpret_cast<f32x4*>(dst + 4) = acc1;
+                if (c8 == 0) a.part_ml[prow] = make_float2(M, L);
             }
         }
-        m_eff = M;
     }
-
-    if (kw != 0) return;
-    const float L = xhalf_sum(l_run);
-    if (q_row >= nq) return;
-
-    if (a.splits == 1) {
-        const float inv = 1.f / L;
-        TOut* Ob = reinterpret_cast<TOut*>(a.o) + ((size_t)bh * nq + q_row) * kHeadDim;
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-            const int d = 8 * g4 + 4 * hh;
-            store4<TOut>(Ob + d, o0[4 * g4] * inv, o0[4 * g4 + 1] * inv, o0[4 * g4 + 2] * inv,
-                         o0[4 * g4 + 3] * inv);
-            store4<TOut>(Ob + 32 + d, o1[4 * g4] * inv, o1[4 * g4 + 1] * inv, o1[4 * g4 + 2] * inv,
-                         o1[4 * g4 + 3] * inv);
-        }
-    } else {
-        const size_t prow = ((size_t)bh * a.splits + split) * nq + q_row;
-        float* Pb = a.part_o + prow * kHeadDim;
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-            const int d = 8 * g4 + 4 * hh;
-            store4<float>(Pb + d, o0[4 * g4], o0[4 * g4 + 1], o0[4 * g4 + 2], o0[4 * g4 + 3]);
-            store4<float>(Pb + 32 + d, o1[4 * g4], o1[4 * g4 + 1], o1[4 * g4 + 2], o1[4 * g4 + 3]);
-        }
-        if (hh == 0) a.part_ml[prow] = make_float2(m_eff, L);
-    }
+    STAMP(4);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -435,8 +618,11 @@ __global__ __launch_bounds__(256) void mha_hd64_combine_kernel(const float* __re
 
 template <typename TIn, typename TOut, int QW, int KW>
 hipError_t launch_fwd(const FwdArgs& a, int bh, hipStream_t stream) {
-    const dim3 grid((a.nq + 32 * QW - 1) / (32 * QW), bh, a.splits);
-    hipLaunchKernelGGL((mha_hd64_fwd_kernel<TIn, TOut, QW, KW>), grid, dim3(64 * QW * KW), 0, stream, a);
+    FwdArgs b = a;
+    b.qtiles = (a.nq + 32 * QW - 1) / (32 * QW);
+    b.bh = bh;
+    const dim3 grid(b.qtiles * bh * a.splits);
+    hipLaunchKernelGGL((mha_hd64_fwd_kernel<TIn, TOut, QW, KW>), grid, dim3(64 * QW * KW), 0, stream, b);
     return hipGetLastError();
 }
 
@@ -445,9 +631,8 @@ hipError_t launch_fwd_shape(const FwdArgs& a, int bh, int qw, int kw, hipStream_
     switch (qw * 8 + kw) {
         case 4 * 8 + 1: return launch_fwd<TIn, TOut, 4, 1>(a, bh, stream);
         case 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2>(a, bh, stream);
-        case 1 * 8 + 4: return launch_fwd<TIn, TOut, 1, 4>(a, bh, stream);
+        case 1 * 8 + 2: return launch_fwd<TIn, TOut, 1, 2>(a, bh, stream);
         case 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2>(a, bh, stream);
-        case 2 * 8 + 4: return launch_fwd<TIn, TOut, 2, 4>(a, bh, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -463,11 +648,14 @@ hipError_t launch_combine(const FwdArgs& a, int bh, hipStream_t stream) {
 }
 
 bool valid_shape(int qw, int kw) {
-    return (qw == 4 && kw == 1) || (qw == 2 && kw == 2) || (qw == 1 && kw == 4) || (qw == 4 && kw == 2) ||
-           (qw == 2 && kw == 4);
+    return (qw == 4 && kw == 1) || (qw == 2 && kw == 2) || (qw == 1 && kw == 2) || (qw == 4 && kw == 2);
 }
 
+unsigned long long* g_stamps = nullptr;  // diagnostic builds (MHA_STAMPS) only
+
 }  // namespace
+
+void set_stamp_buffer(void* p) { g_stamps = reinterpret_cast<unsigned long long*>(p); }
 
 size_t split_workspace_bytes(const Call& c, int splits) {
     if (splits <= 1) return 0;
@@ -524,6 +712,7 @@ hipError_t launch_attention(const Call& c, InType in, OutType out, void* workspa
     a.nkv = c.nkv;
     a.splits = p.splits;
     a.tiles_per_split = p.tiles_per_split;
+    a.stamps = g_stamps;
     if (p.splits > 1) {
         const size_t rows = (size_t)c.batch * c.heads * p.splits * c.nq;
         a.part_o = reinterpret_cast<float*>(workspace);

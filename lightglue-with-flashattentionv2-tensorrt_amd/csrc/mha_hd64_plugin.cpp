@@ -317,7 +317,7 @@ const char* mha_hd64_last_error(void) { return g_last_error.c_str(); }
 void mha_hd64_set_abort_on_error(int32_t enable) { g_abort_on_error = enable != 0; }
 const char* mha_hd64_build_info(void) {
     return "mha_hd64: gfx950 (CDNA4) HIP kernels, v_mfma_f32_32x32x16_f16 + ds_read_b64_tr_b16; "
-           "variants fp16->fp16, fp16->fp32, fp32->fp32; workgroups (q,kv waves) 4x1 2x2 1x4 4x2 2x4; split-KV combine";
+           "variants fp16->fp16, fp16->fp32, fp32->fp32; workgroups (q,kv waves) 4x1 2x2 1x2 4x2; software-pipelined QK(t+1)|softmax(t); split-KV combine";
 }
 
 // Test/bench hook (not part of include/mha_hd64.h): launch with a forced plan
@@ -341,6 +341,9 @@ int32_t mha_hd64_launch_forced(const void* q, const void* k, const void* v, void
                                                     phase_mask),
                          __FILE__, __LINE__);
 }
+
+// Diagnostic hook: per-workgroup timestamp buffer for -DMHA_STAMPS builds (ignored otherwise).
+void mha_hd64_set_stamp_buffer(void* p) { mha_hd64::set_stamp_buffer(p); }
 
 // Plan query hook for tests/bench: fills {q_waves, kv_waves, splits, tiles_per_split}; returns workspace bytes.
 size_t mha_hd64_plan(int32_t batch, int32_t heads, int32_t nq, int32_t nkv, size_t ws_bytes, int32_t* out4) {
