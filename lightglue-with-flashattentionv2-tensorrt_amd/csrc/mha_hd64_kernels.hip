@@ -253,19 +253,20 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     const int kw = wave / QW;
     const int nq = a.nq, nkv = a.nkv;
     // XCD-aware order (T1): the dispatcher deals consecutive blocks round-robin over the 8 XCDs;
-    // renumber so that the blocks sharing one XCD are consecutive query blocks of the same
-    // (batch, head, split), i.e. read the same K/V through the same L2. Bijective for any count.
+    // renumber (bijectively, any count) so that the blocks sharing one XCD are consecutive in
+    // j = split + S*(qtile + qtiles*bh): the KV splits and neighbouring query blocks of one
+    // (batch, head) run on one XCD, read its K/V through one L2 and leave their split partials
+    // there for the combine kernel (which maps its blocks to the same XCD).
     int qtile, bh, split;
     {
         const int T = gridDim.x, L = blockIdx.x;
         const int q8 = T >> 3, r8 = T & 7, xcd = L & 7;
         const int j = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
-        qtile = j % a.qtiles;
-        const int rest = j / a.qtiles;
-        bh = rest % a.bh;
-        split = rest / a.bh;
+        split = j % a.splits;
+        const int g = j / a.splits;
+        qtile = g % a.qtiles;
+        bh = g / a.qtiles;
     }
-
     const TIn* Qb = reinterpret_cast<const TIn*>(a.q) + (size_t)bh * nq * kHeadDim;
     const TIn* Kb = reinterpret_cast<const TIn*>(a.k) + (size_t)bh * nkv * kHeadDim;
     const TIn* Vb = reinterpret_cast<const TIn*>(a.v) + (size_t)bh * nkv * kHeadDim;
@@ -586,34 +587,72 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
 
 // ----------------------------------------------------------------------------------------
 // Split-KV combine: O = Σ_s w_s O_s / Σ_s w_s l_s with w_s = exp2(m_s - M) (m in log2 units).
-// One thread per (row, 4-dim chunk).
+// One thread per (row, 4-dim chunk). Block b serves XCD b % 8: it combines rows whose partials
+// the main kernel produced on that same XCD (same bijective block order), so the reads hit L2.
+// All partials of a row are loaded in one round trip (S <= kMaxSplits).
 // ----------------------------------------------------------------------------------------
+constexpr int kMaxSplits = 16;
+
+struct CombineArgs {
+    const float* part_o;
+    const float2* part_ml;
+    void* out;
+    int nq;
+    int splits;
+    int qtiles;      // query blocks per (batch, head) of the main kernel
+    int block_m;     // rows per query block
+    int groups;      // qtiles * bh
+    int main_blocks; // grid of the main kernel (groups * splits)
+    int per_xcd;     // combine blocks per XCD
+};
+
+__device__ __forceinline__ int xcd_j_begin(int T, int x) {
+    const int q8 = T >> 3, r8 = T & 7;
+    return x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+}
+
 template <typename TOut>
-__global__ __launch_bounds__(256) void mha_hd64_combine_kernel(const float* __restrict__ part_o,
-                                                               const float2* __restrict__ part_ml,
-                                                               TOut* __restrict__ out, int rows, int nq,
-                                                               int splits) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    const int row = idx >> 4;  // = bh * nq + q
-    if (row >= rows) return;
-    const int chunk = idx & 15;
-    const int bh = row / nq, q = row - bh * nq;
-    const size_t base = (size_t)bh * splits * nq + q;
+__global__ __launch_bounds__(256) void mha_hd64_combine_kernel(CombineArgs c) {
+    const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
+    // Groups (query blocks) whose first split block the main kernel ran on XCD x.
+    const int jlo = xcd_j_begin(c.main_blocks, x), jhi = xcd_j_begin(c.main_blocks, x + 1);
+    const int glo = (jlo + c.splits - 1) / c.splits, ghi = min(c.groups, (jhi + c.splits - 1) / c.splits);
+    const int local = k * 256 + threadIdx.x;
+    const int lrow = local >> 4;
+    const int g = glo + lrow / c.block_m;
+    if (g >= ghi) return;
+    const int chunk = local & 15;
+    const int bh = g / c.qtiles, qt = g - bh * c.qtiles;
+    const int q = qt * c.block_m + lrow % c.block_m;
+    if (q >= c.nq) return;
+    const size_t base = (size_t)bh * c.splits * c.nq + q;
+    float2 ml[kMaxSplits];
+    f32x4 v[kMaxSplits];
+#pragma unroll
+    for (int s = 0; s < kMaxSplits; ++s) {
+        if (s < c.splits) {
+            const size_t pr = base + (size_t)s * c.nq;
+            ml[s] = c.part_ml[pr];
+            v[s] = *reinterpret_cast<const f32x4*>(c.part_o + pr * kHeadDim + chunk * 4);
+        }
+    }
     float M = -INFINITY;
-    for (int s = 0; s < splits; ++s) M = fmaxf(M, part_ml[base + (size_t)s * nq].x);
+#pragma unroll
+    for (int s = 0; s < kMaxSplits; ++s)
+        if (s < c.splits) M = fmaxf(M, ml[s].x);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     float L = 0.f;
-    for (int s = 0; s < splits; ++s) {
-        const size_t pr = base + (size_t)s * nq;
-        const float2 ml = part_ml[pr];
-        const float w = (ml.x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml.x - M);
-        L += w * ml.y;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(part_o + pr * kHeadDim + chunk * 4);
-        acc += w * v;
+#pragma unroll
+    for (int s = 0; s < kMaxSplits; ++s) {
+        if (s < c.splits) {
+            const float w = (ml[s].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[s].x - M);
+            L += w * ml[s].y;
+            acc += w * v[s];
+        }
     }
     const float inv = 1.f / L;
-    store4<TOut>(out + (size_t)row * kHeadDim + chunk * 4, acc[0] * inv, acc[1] * inv, acc[2] * inv,
-                 acc[3] * inv);
+    TOut* out = reinterpret_cast<TOut*>(c.out) + ((size_t)bh * c.nq + q) * kHeadDim + chunk * 4;
+    store4<TOut>(out, acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
 }
 
 template <typename TIn, typename TOut, int QW, int KW>
@@ -638,12 +677,21 @@ hipError_t launch_fwd_shape(const FwdArgs& a, int bh, int qw, int kw, hipStream_
 }
 
 template <typename TOut>
-hipError_t launch_combine(const FwdArgs& a, int bh, hipStream_t stream) {
-    const int rows = bh * a.nq;
-    const int threads = rows * 16;
-    const dim3 grid((threads + 255) / 256);
-    hipLaunchKernelGGL((mha_hd64_combine_kernel<TOut>), grid, dim3(256), 0, stream, a.part_o, a.part_ml,
-                       reinterpret_cast<TOut*>(a.o), rows, a.nq, a.splits);
+hipError_t launch_combine(const FwdArgs& a, int bh, int qw, hipStream_t stream) {
+    CombineArgs c{};
+    c.part_o = a.part_o;
+    c.part_ml = a.part_ml;
+    c.out = a.o;
+    c.nq = a.nq;
+    c.splits = a.splits;
+    c.block_m = 32 * qw;
+    c.qtiles = (a.nq + c.block_m - 1) / c.block_m;
+    c.groups = c.qtiles * bh;
+    c.main_blocks = c.groups * a.splits;
+    // Rows per XCD: at most ceil(groups / 8) + 1 groups (the split ranges may straddle).
+    const int max_groups_per_xcd = (c.groups + 7) / 8 + 1;
+    c.per_xcd = (max_groups_per_xcd * c.block_m * 16 + 255) / 256;
+    hipLaunchKernelGGL((mha_hd64_combine_kernel<TOut>), dim3(8 * c.per_xcd), dim3(256), 0, stream, c);
     return hipGetLastError();
 }
 
@@ -679,7 +727,7 @@ LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves, int forc
     const int qtiles = (c.nq + 32 * qw - 1) / (32 * qw);
     const int super_total = (c.nkv + 64 * kw - 1) / (64 * kw);
     int want = force_splits > 0 ? force_splits : (256 + qtiles * bh - 1) / (qtiles * bh);
-    want = std::max(1, std::min(want, super_total));
+    want = std::max(1, std::min(std::min(want, super_total), kMaxSplits));
     LaunchPlan p{};
     p.q_waves = qw;
     p.kv_waves = kw;
@@ -730,7 +778,8 @@ hipError_t launch_attention(const Call& c, InType in, OutType out, void* workspa
         }
     }
     if (e != hipSuccess || p.splits == 1 || !(phase_mask & 2)) return e;
-    return (out == OutType::F16) ? launch_combine<f16>(a, bh, stream) : launch_combine<float>(a, bh, stream);
+    return (out == OutType::F16) ? launch_combine<f16>(a, bh, p.q_waves, stream)
+                                 : launch_combine<float>(a, bh, p.q_waves, stream);
 }
 
 }  // namespace mha_hd64
