@@ -62,7 +62,7 @@ struct FwdArgs {
     const void* k;
     const void* v;
     void* o;
-    float* part_o;   // [bh][splits][nq][64] fp32, unnormalised (splits > 1 only)
+    void* part_o;    // [bh][splits][nq][64] O_s / l_s in TOut precision (splits > 1 only)
     float2* part_ml; // [bh][splits][nq] (m in log2 units, l)
     int nq;
     int nkv;
@@ -109,11 +109,6 @@ __device__ __forceinline__ float xhalf_max(float x) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
-__device__ __forceinline__ float xhalf_sum(float x) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);  // same order in both halves
-}
-
 __device__ __forceinline__ float tree_max(const f32x16& a, const f32x16& b) {
     float t[16];
 #pragma unroll
@@ -124,17 +119,6 @@ __device__ __forceinline__ float tree_max(const f32x16& a, const f32x16& b) {
         for (int i = 0; i < w; ++i) t[i] = fmaxf(t[i], t[i + w]);
     return t[0];
 }
-__device__ __forceinline__ float tree_sum(const f32x16& a, const f32x16& b) {
-    float t[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t[i] = a[i] + b[i];
-#pragma unroll
-    for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-        for (int i = 0; i < w; ++i) t[i] = t[i] + t[i + w];
-    return t[0];
-}
-
 // LDS accesses through an explicit address-space-3 base and 32-bit byte offsets, so the
 // compiler folds the compile-time part of every address into the DS instruction's offset field.
 typedef __attribute__((address_space(3))) char lds_char;
@@ -181,7 +165,8 @@ __device__ __forceinline__ f32x16 splat16(float x) {
 #define ABL_NO_SOFTMAX 8
 #define ABL_NO_PV 16
 #define ABL_NO_QK 32
-#define ABL_QK_NO_LDS_DEP 64
+#define ABL_NO_GLOAD 64   // no K/V/Q global loads (LDS and Q hold garbage)
+#define ABL_NO_STORE 128  // no output / partial stores
 __device__ __forceinline__ void keep_live(const f16x8& x) { asm volatile("" ::"v"(x)); }
 
 // In-kernel timestamps (diagnostic build -DMHA_STAMPS only): s_memtime after draining memory.
@@ -200,6 +185,13 @@ __device__ __forceinline__ void keep_live(const f16x8& x) { asm volatile("" ::"v
     } while (0)
 #endif
 
+#ifndef MHA_ST_AUX
+#define MHA_ST_AUX 0    // cache policy bits of the output stores (2 = nt, 16 = sc1)
+#endif
+#ifndef MHA_PART_AUX
+#define MHA_PART_AUX 0  // cache policy bits of the split-partial stores
+#endif
+
 constexpr float kMaskBias = -65504.f;  // fp16 lowest: a masked key's score, exp2 -> 0
 constexpr float kEmptyMax = -30000.f;  // tile max below this: every key of the tile was masked
 
@@ -209,6 +201,17 @@ constexpr float kEmptyMax = -30000.f;  // tile max below this: every key of the 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+}
+// 8 consecutive output values (dims c8..c8+7 of one row) as one (f16) or two (f32) 16-B stores.
+template <typename T, int AUX>
+__device__ __forceinline__ void store8(__amdgpu_buffer_rsrc_t rs, unsigned voff, f32x4 a, f32x4 b) {
+    if constexpr (sizeof(T) == 2) {
+        const f16x8 h = f16x8{(f16)a[0], (f16)a[1], (f16)a[2], (f16)a[3], (f16)b[0], (f16)b[1], (f16)b[2], (f16)b[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), rs, voff, 0, AUX);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), rs, voff, 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), rs, voff + 16, 0, AUX);
+    }
 }
 __device__ __forceinline__ void bload8(Raw8<f16>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff) {
     r.x = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
@@ -289,6 +292,11 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     // of latency cover for first-touch MALL/HBM reads) while set t+2 is written to LDS.
     Raw8<TIn> stgA[NLOAD], stgB[NLOAD];
     auto issue = [&](int it, Raw8<TIn>(&stg)[NLOAD]) {
+        if (MHA_ABL & ABL_NO_GLOAD) {
+#pragma unroll
+            for (int i = 0; i < NLOAD; ++i) stg[i] = Raw8<TIn>{};
+            return;
+        }
         const unsigned soff = (unsigned)(st_begin + it) * SUPER * kHeadDim * SZ;
 #pragma unroll
         for (int i = 0; i < NLOAD; ++i) {
@@ -314,17 +322,18 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         Raw8<TIn> t;
-        bload8(t, q_rs, (unsigned)(q_row * kHeadDim + 16 * s + 8 * hh) * SZ, 0);
+        if (MHA_ABL & ABL_NO_GLOAD) t = Raw8<TIn>{};
+        else bload8(t, q_rs, (unsigned)(q_row * kHeadDim + 16 * s + 8 * hh) * SZ, 0);
         const f16x8 h = to_f16(t);
 #pragma unroll
         for (int e = 0; e < 8; ++e) qf[s][e] = (f16)((float)h[e] * kScaleLog2);
     }
 
-    // Prologue: stages 0 and 1 (super-tiles 0 and 1); super-tile 2 in flight in set A.
+    // Prologue: stage 0 is published first so QKᵀ(0) starts while stage 1 is still in flight
+    // (stage 1 is written and published right after it); super-tile 2 goes in flight in set A.
     if (n_iter > 0) issue(0, stgA);
     if (n_iter > 1) issue(1, stgB);
     if (n_iter > 0) write(0, stgA);
-    if (n_iter > 1) write(1, stgB);
     if (n_iter > 2) issue(2, stgA);
     __syncthreads();
     STAMP(1);
@@ -342,7 +351,14 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     const unsigned v_addr1 = v_lane + 64 * (1 - vb) + (kw * 2 + 1) * kTileBytes;  // dims 32..63
 
     float m_run = 0.f;        // reference max of this lane's query, log2 units (s·c)
-    float l_run = 0.f;        // running sum, in-lane partial (the two halves hold disjoint keys)
+    // Row sums on the matrix pipe: l_acc = ones_sel · P over every k-step (16x16x32 MFMA), so the
+    // 31 adds per tile leave the vector pipe. P (the 32x32x16 B operand) read as a 16x16x32 B
+    // operand puts query n (lanes 0-15, 32-47) and n+16 (lanes 16-31, 48-63) in column n; the
+    // selector row m takes k-group g when ((m>>2)&1) == (g&1), so lane l's four D rows all hold
+    // the sum of query l&31 over the step's 16 keys (both half-waves) — the lane's own query.
+    const f16 sel = (((lane & 15) >> 2) & 1) == ((lane >> 4) & 1) ? (f16)1.f : (f16)0.f;
+    const f16x8 a_sum = f16x8{sel, sel, sel, sel, sel, sel, sel, sel};
+    f32x4 l_acc = {0.f, 0.f, 0.f, 0.f};
     // Bias k-step of the QKᵀ chains: A (key side) = [1, 1, mask] per key row, B (query side) =
     // [-m_hi, -m_lo, 1] per query, in k-slots 0..2 of the lower half-wave (zeros elsewhere).
     // One extra MFMA per chain adds -m (fp16 hi + lo, error ~|m|·2^-22) and the tail mask, so
@@ -358,41 +374,36 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     };
     f32x16 o0 = {}, o1 = {};  // Oᵀ tiles: dims 0..31 and 32..63, query on the lane
 
-    // QKᵀ of super-tile t (this wave's tile), scores relative to m_run.
-    // QKᵀ of the tile in stage kstage: scores s·c - m (log2 units), masked keys at ~-65504.
-    auto qk = [&](unsigned kstage, const f16x8& ab0, const f16x8& ab1, f32x16& s0, f32x16& s1) {
-        f16x8 kf[8];
+    // K fragments of the tile in stage kstage (A operand of Sᵀ = K·Qᵀ, 8 x ds_read_b128).
+    auto read_k = [&](unsigned kstage, f16x8(&kf)[8]) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const unsigned ka = k_addr[s] + kstage;
             kf[2 * s] = lds_read16(lds, ka);
             kf[2 * s + 1] = lds_read16(lds, ka + 32 * 128);
         }
+    };
+    // QKᵀ chain step i (0..9) of the tile: i = 0,1 are the bias k-steps of the two 32-key halves,
+    // then K·Qᵀ over the 4 dim k-steps alternating halves. Scores s·c - m (log2 units), masked
+    // keys at ~-65504. Split per MFMA so the caller can interleave vector work between them.
+    auto qk_step = [&](int i, const f16x8(&kf)[8], const f16x8& ab0, const f16x8& ab1, f32x16& s0, f32x16& s1) {
         const f32x16 zero = {};
         if (MHA_ABL & ABL_NO_QK) {
-#pragma unroll
-            for (int s = 0; s < 8; ++s) keep_live(kf[s]);
-            s0 = zero;
-            s1 = zero;
+            if (i == 0) s0 = zero;
+            if (i == 1) s1 = zero;
+            if (i >= 2) keep_live(kf[i - 2]);
             return;
         }
-        s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab0, b_bias, zero, 0, 0, 0);
-        s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab1, b_bias, zero, 0, 0, 0);
-        if (MHA_ABL & ABL_QK_NO_LDS_DEP) {
+        if (i == 0) s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab0, b_bias, zero, 0, 0, 0);
+        else if (i == 1) s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab1, b_bias, zero, 0, 0, 0);
+        else if ((i & 1) == 0) s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[i - 2], qf[(i - 2) >> 1], s0, 0, 0, 0);
+        else s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[i - 2], qf[(i - 2) >> 1], s1, 0, 0, 0);
+    };
+    auto qk = [&](unsigned kstage, const f16x8& ab0, const f16x8& ab1, f32x16& s0, f32x16& s1) {
+        f16x8 kf[8];
+        read_k(kstage, kf);
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(qf[(s + 1) & 3], qf[s], s0, 0, 0, 0);
-                s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(qf[(s + 2) & 3], qf[s], s1, 0, 0, 0);
-            }
-#pragma unroll
-            for (int s = 0; s < 8; ++s) keep_live(kf[s]);
-            return;
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s], qf[s], s0, 0, 0, 0);
-            s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s + 1], qf[s], s1, 0, 0, 0);
-        }
+        for (int i = 0; i < 10; ++i) qk_step(i, kf, ab0, ab1, s0, s1);
     };
     // Tail mask (reference: last KV tile only, …fp16out.cu:475-494): the bias A operand of the
     // tile carries kMaskBias in k-slot 2 for key rows >= nkv. Only the last super-tile of the
@@ -409,11 +420,16 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     auto next_stage = [](int st) { return st == NSTAGE - 1 ? 0 : st + 1; };
     // Step `it` writes super-tile it+2 from set `wr` and issues super-tile it+3 into set `is`.
     auto step = [&](int it, f32x16& c0, f32x16& c1, float mxc, f32x16& n0, f32x16& n1, float& mxn,
-                    auto has_next_c, bool mask_next, Raw8<TIn>(&wr)[NLOAD], Raw8<TIn>(&is)[NLOAD]) {
+                    auto has_next_c, bool mask_next, Raw8<TIn>(&wr)[NLOAD], Raw8<TIn>(&is)[NLOAD],
+                    bool may_issue) {
         constexpr bool HAS_NEXT = decltype(has_next_c)::value;
         const int st_nxt = next_stage(st_cur);
         const int st_fill = next_stage(st_nxt);
-        if (!(MHA_ABL & ABL_NO_REFILL) && it + 3 < n_iter) issue(it + 3, is);
+        // In the steady loop the refill is unconditional (may_issue = true at compile time): a load
+        // past this split's last super-tile is never written to LDS, and past nkv the buffer
+        // descriptor returns zeros. A conditional load would make the compiler's vmcnt analysis
+        // drain every load at the next LDS write (a one-step prefetch instead of two).
+        if (!(MHA_ABL & ABL_NO_REFILL) && may_issue) issue(it + 3, is);
 
         // online-softmax decision for tile `it` (first tile: set the max exactly; later tiles:
         // move it only when some query's tile max exceeds it by > kRescaleThr)
@@ -424,28 +440,65 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
             const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-d);
             o0 *= alpha;
             o1 *= alpha;
-            l_run *= alpha;
+            l_acc *= alpha;
             m_run += d;
             c0 -= d;
             c1 -= d;
             set_bias();
         }
 
-        // phase A: QKᵀ(it+1) on the matrix pipe ‖ softmax(it) on the vector pipe
-        if constexpr (HAS_NEXT) {
-            if (mask_next)
-                qk((unsigned)st_nxt * STAGE_BYTES, a_bias_tile(it + 1, 0), a_bias_tile(it + 1, 1), n0, n1);
-            else
-                qk((unsigned)st_nxt * STAGE_BYTES, a_bias, a_bias, n0, n1);
-        }
-        if (!(MHA_ABL & (ABL_NO_EXP | ABL_NO_SOFTMAX))) {
+        // Fragment reads first: K of tile it+1 (phase A) and Vᵀ of tile it (phase B); both stages
+        // are complete since the last barrier, and the reads land while the bias MFMAs run.
+        f16x8 kf[8];
+        if constexpr (HAS_NEXT) read_k((unsigned)st_nxt * STAGE_BYTES, kf);
+        // (8-wave workgroups with fp32 staging registers read Vᵀ in phase B instead: the early
+        // reads' 32 VGPRs would spill there.)
+        constexpr bool kEarlyV = !(NT == 512 && SZ == 4);
+        f16x8 vfa[2][2], vfb[2][2];
+        auto read_v = [&]() {
+            const unsigned va0 = v_addr0 + (unsigned)st_cur * STAGE_BYTES;
+            const unsigned va1 = v_addr1 + (unsigned)st_cur * STAGE_BYTES;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                c0[i] = __builtin_amdgcn_exp2f(c0[i]);
-                c1[i] = __builtin_amdgcn_exp2f(c1[i]);
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    const unsigned rowc = 128 * (32 * j + 16 * ss);
+                    vfa[j][ss] = cat8(tr_read(lds, va0 + rowc), tr_read(lds, va0 + rowc + 8 * 128));
+                    vfb[j][ss] = cat8(tr_read(lds, va1 + rowc), tr_read(lds, va1 + rowc + 8 * 128));
+                }
+        };
+        if constexpr (kEarlyV && !HAS_NEXT) read_v();
+
+        // phase A: QKᵀ(it+1) on the matrix pipe ‖ exp(it) on the vector pipe, pinned as one MFMA
+        // followed by three v_exp_f32 per gap (8 + 3·8 issue cycles fill the MFMA's 32).
+        auto exp_at = [&](int e) {
+            if (MHA_ABL & (ABL_NO_EXP | ABL_NO_SOFTMAX)) return;
+            if (e < 16) c0[e] = __builtin_amdgcn_exp2f(c0[e]);
+            else c1[e - 16] = __builtin_amdgcn_exp2f(c1[e - 16]);
+        };
+        if constexpr (HAS_NEXT) {
+            const f16x8 ab0 = mask_next ? a_bias_tile(it + 1, 0) : a_bias;
+            const f16x8 ab1 = mask_next ? a_bias_tile(it + 1, 1) : a_bias;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 10; ++i) {
+                qk_step(i, kf, ab0, ab1, n0, n1);
+                // LDS traffic spread over the MFMA phase instead of bursts at the step's ends:
+                // Vᵀ reads queue behind the K reads; the refill of stage it+2 (free since the
+                // last barrier) lands mid-phase.
+                if (kEarlyV && i == 2) read_v();
+                if (i == 6 && !(MHA_ABL & ABL_NO_REFILL) && it + 2 < n_iter) write(st_fill, wr);
+                exp_at(3 * i);
+                exp_at(3 * i + 1);
+                exp_at(3 * i + 2);
+                __builtin_amdgcn_sched_barrier(0);
             }
+            exp_at(30);
+            exp_at(31);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 32; ++e) exp_at(e);
         }
-        if (!(MHA_ABL & ABL_NO_SOFTMAX)) l_run += tree_sum(c0, c1);
         f16x8 p[2][2];  // P (f16) as the B operand: registers 8ss..8ss+7 of a 32x32 tile = k-step ss
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -455,31 +508,29 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
             p[1][1][e] = (f16)c1[8 + e];
         }
 
-        // phase B: Oᵀ += Vᵀ·Pᵀ (it) on the matrix pipe ‖ row max (it+1)
-        const unsigned va0 = v_addr0 + (unsigned)st_cur * STAGE_BYTES;
-        const unsigned va1 = v_addr1 + (unsigned)st_cur * STAGE_BYTES;
+        // phase B: Oᵀ += Vᵀ·Pᵀ (it) and the row sums on the matrix pipe ‖ row max (it+1)
+        if constexpr (!kEarlyV) read_v();
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
-                const unsigned rowc = 128 * (32 * j + 16 * ss);
-                const f16x8 va = cat8(tr_read(lds, va0 + rowc), tr_read(lds, va0 + rowc + 8 * 128));
-                const f16x8 vb8 = cat8(tr_read(lds, va1 + rowc), tr_read(lds, va1 + rowc + 8 * 128));
                 if (MHA_ABL & ABL_NO_PV) {
-                    keep_live(va);
-                    keep_live(vb8);
+                    keep_live(vfa[j][ss]);
+                    keep_live(vfb[j][ss]);
                     keep_live(p[j][ss]);
                 } else {
-                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, p[j][ss], o0, 0, 0, 0);
-                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vb8, p[j][ss], o1, 0, 0, 0);
+                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa[j][ss], p[j][ss], o0, 0, 0, 0);
+                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb[j][ss], p[j][ss], o1, 0, 0, 0);
                 }
+                if (!(MHA_ABL & ABL_NO_SOFTMAX))
+                    l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, p[j][ss], l_acc, 0, 0, 0);
             }
         if constexpr (HAS_NEXT) {
             if (MHA_ABL & ABL_NO_SOFTMAX) mxn = 0.f;
             else mxn = xhalf_max(tree_max(n0, n1));
         }
 
-        if (!(MHA_ABL & ABL_NO_REFILL) && it + 2 < n_iter) write(st_fill, wr);
+        if (!HAS_NEXT && !(MHA_ABL & ABL_NO_REFILL) && it + 2 < n_iter) write(st_fill, wr);
         if (!(MHA_ABL & ABL_NO_BARRIER)) __syncthreads();
         st_cur = st_nxt;
     };
@@ -496,23 +547,27 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
             qk(0u, a_bias, a_bias, sA0, sA1);
         mxA = xhalf_max(tree_max(sA0, sA1));
     }
+    if (n_iter > 1) {
+        write(1, stgB);
+        __syncthreads();
+    }
     int it = 0;
     // Steady state: tiles it+1 and it+2 exist and neither is the (possibly partial) last one.
     for (; it + 3 < n_iter; it += 2) {
-        step(it, sA0, sA1, mxA, sB0, sB1, mxB, T_{}, false, stgA, stgB);
-        step(it + 1, sB0, sB1, mxB, sA0, sA1, mxA, T_{}, false, stgB, stgA);
+        step(it, sA0, sA1, mxA, sB0, sB1, mxB, T_{}, false, stgA, stgB, true);
+        step(it + 1, sB0, sB1, mxB, sA0, sA1, mxA, T_{}, false, stgB, stgA, true);
     }
     // Tail (at most 3 iterations): same step with the mask flag live; scores and the pending
     // staging set move back to A after each step.
     for (; it + 1 < n_iter; ++it) {
-        step(it, sA0, sA1, mxA, sB0, sB1, mxB, T_{}, tail && (it + 2 == n_iter), stgA, stgB);
+        step(it, sA0, sA1, mxA, sB0, sB1, mxB, T_{}, tail && (it + 2 == n_iter), stgA, stgB, it + 3 < n_iter);
         sA0 = sB0;
         sA1 = sB1;
         mxA = mxB;
 #pragma unroll
         for (int i = 0; i < NLOAD; ++i) stgA[i] = stgB[i];
     }
-    if (it < n_iter) step(it, sA0, sA1, mxA, sB0, sB1, mxB, F_{}, false, stgA, stgB);
+    if (it < n_iter) step(it, sA0, sA1, mxA, sB0, sB1, mxB, F_{}, false, stgA, stgB, false);
     STAMP(2);
 
     // ---- epilogue ----
@@ -521,7 +576,7 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     // chunks (a wave stores complete rows: coalesced, few store instructions).
     // A wave that saw no key (all of its tiles past nkv) gets m = -inf (weight 0). The test uses
     // the cross-half total: the halves hold disjoint keys but the SAME query's m and O dims.
-    const float L_w = xhalf_sum(l_run);
+    const float L_w = l_acc[0];  // the row-sum MFMA already spans both half-waves
     const float m_w = (L_w > 0.f) ? m_run : -INFINITY;
     constexpr int OROW = 68;  // fp32 row pitch in LDS: 64 dims + 4 pad (rows r, r+1 on different banks)
     float* ol = reinterpret_cast<float*>(smem);     // [KW][BLOCK_M][OROW]
@@ -542,8 +597,14 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     __syncthreads();
     STAMP(3);
 
-    // Thread -> (row, chunk of 8 dims); 8 threads per row, NT/8 rows per pass.
+    // Thread -> (row, chunk of 8 dims); 8 threads per row, NT/8 rows per pass. Stores are 16-B
+    // buffer stores through per-head descriptors (cache policy MHA_ST_AUX / MHA_PART_AUX).
     const int q_base = qtile * BLOCK_M;
+    const __amdgpu_buffer_rsrc_t o_rs =
+        make_rsrc(reinterpret_cast<TOut*>(a.o) + (size_t)bh * nq * kHeadDim, (unsigned)(nq * kHeadDim * sizeof(TOut)));
+    const __amdgpu_buffer_rsrc_t po_rs =
+        make_rsrc(reinterpret_cast<TOut*>(a.part_o) + (size_t)bh * a.splits * nq * kHeadDim,
+                  (unsigned)(a.splits * nq * kHeadDim * sizeof(TOut)));
 #pragma unroll
     for (int pass = 0; pass < (BLOCK_M * 8) / NT; ++pass) {
         const int idx = pass * NT + tid;
@@ -567,18 +628,18 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
             acc0 += w * *reinterpret_cast<const f32x4*>(src);
             acc1 += w * *reinterpret_cast<const f32x4*>(src + 4);
         }
-        if (q < nq) {
+        if (q < nq && !(MHA_ABL & ABL_NO_STORE)) {
             if (a.splits == 1) {
                 const float inv = 1.f / L;
-                TOut* dst = reinterpret_cast<TOut*>(a.o) + ((size_t)bh * nq + q) * kHeadDim + c8;
-                store4<TOut>(dst, acc0[0] * inv, acc0[1] * inv, acc0[2] * inv, acc0[3] * inv);
-                store4<TOut>(dst + 4, acc1[0] * inv, acc1[1] * inv, acc1[2] * inv, acc1[3] * inv);
+                store8<TOut, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c8) * sizeof(TOut)), acc0 * inv, acc1 * inv);
             } else {
-                const size_t prow = ((size_t)bh * a.splits + split) * nq + q;
-                float* dst = a.part_o + prow * kHeadDim + c8;
-                *reinterpret_cast<f32x4*>(dst) = acc0;
-                *reinterpret_cast<f32x4*>(dst + 4) = acc1;
-                if (c8 == 0) a.part_ml[prow] = make_float2(M, L);
+                // Partial O_s / l_s in the output precision (fp16 halves the partial traffic of
+                // the fp16 path; the fp32-output path keeps fp32), merged with weights l_s·2^(m_s-M).
+                const unsigned prow = (unsigned)(split * nq + q);
+                const float inv = (L > 0.f) ? 1.f / L : 0.f;
+                store8<TOut, MHA_PART_AUX>(po_rs, prow * (unsigned)(kHeadDim * sizeof(TOut)) + c8 * (unsigned)sizeof(TOut),
+                                           acc0 * inv, acc1 * inv);
+                if (c8 == 0) a.part_ml[((size_t)bh * a.splits) * nq + prow] = make_float2(M, L);
             }
         }
     }
@@ -586,15 +647,15 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
 }
 
 // ----------------------------------------------------------------------------------------
-// Split-KV combine: O = Σ_s w_s O_s / Σ_s w_s l_s with w_s = exp2(m_s - M) (m in log2 units).
-// One thread per (row, 4-dim chunk). Block b serves XCD b % 8: it combines rows whose partials
-// the main kernel produced on that same XCD (same bijective block order), so the reads hit L2.
-// All partials of a row are loaded in one round trip (S <= kMaxSplits).
+// Split-KV combine: O = Σ_s w_s Ô_s / Σ_s w_s with w_s = l_s·2^(m_s - M) (m in log2 units) and
+// Ô_s = O_s / l_s the partial as stored (TOut precision). One thread per (row, 4-dim chunk).
+// Block b serves XCD b % 8: it combines rows whose partials the main kernel produced on that same XCD (same bijective block order), so the reads hit L2. All
+// partials of a row are loaded in one round trip (S <= kMaxSplits).
 // ----------------------------------------------------------------------------------------
 constexpr int kMaxSplits = 16;
 
 struct CombineArgs {
-    const float* part_o;
+    const void* part_o;
     const float2* part_ml;
     void* out;
     int nq;
@@ -609,6 +670,16 @@ struct CombineArgs {
 __device__ __forceinline__ int xcd_j_begin(int T, int x) {
     const int q8 = T >> 3, r8 = T & 7;
     return x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+}
+
+template <typename T>
+__device__ __forceinline__ f32x4 load4f(const T* p) {
+    if constexpr (sizeof(T) == 2) {
+        const f16x4 h = *reinterpret_cast<const f16x4*>(p);
+        return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+    } else {
+        return *reinterpret_cast<const f32x4*>(p);
+    }
 }
 
 template <typename TOut>
@@ -626,6 +697,7 @@ __global__ __launch_bounds__(256) void mha_hd64_combine_kernel(CombineArgs c) {
     const int q = qt * c.block_m + lrow % c.block_m;
     if (q >= c.nq) return;
     const size_t base = (size_t)bh * c.splits * c.nq + q;
+    const TOut* po = reinterpret_cast<const TOut*>(c.part_o);
     float2 ml[kMaxSplits];
     f32x4 v[kMaxSplits];
 #pragma unroll
@@ -633,7 +705,7 @@ __global__ __launch_bounds__(256) void mha_hd64_combine_kernel(CombineArgs c) {
         if (s < c.splits) {
             const size_t pr = base + (size_t)s * c.nq;
             ml[s] = c.part_ml[pr];
-            v[s] = *reinterpret_cast<const f32x4*>(c.part_o + pr * kHeadDim + chunk * 4);
+            v[s] = load4f<TOut>(po + pr * kHeadDim + chunk * 4);
         }
     }
     float M = -INFINITY;
@@ -645,8 +717,8 @@ __global__ __launch_bounds__(256) void mha_hd64_combine_kernel(CombineArgs c) {
 #pragma unroll
     for (int s = 0; s < kMaxSplits; ++s) {
         if (s < c.splits) {
-            const float w = (ml[s].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[s].x - M);
-            L += w * ml[s].y;
+            const float w = (ml[s].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[s].x - M) * ml[s].y;
+            L += w;
             acc += w * v[s];
         }
     }
@@ -708,7 +780,7 @@ void set_stamp_buffer(void* p) { g_stamps = reinterpret_cast<unsigned long long*
 size_t split_workspace_bytes(const Call& c, int splits) {
     if (splits <= 1) return 0;
     const size_t rows = (size_t)c.batch * c.heads * splits * c.nq;
-    const size_t o_bytes = rows * kHeadDim * sizeof(float);
+    const size_t o_bytes = rows * kHeadDim * sizeof(float);  // fp32 bound (fp16 partials use half)
     return o_bytes + rows * sizeof(float2);
 }
 
@@ -763,7 +835,7 @@ hipError_t launch_attention(const Call& c, InType in, OutType out, void* workspa
     a.stamps = g_stamps;
     if (p.splits > 1) {
         const size_t rows = (size_t)c.batch * c.heads * p.splits * c.nq;
-        a.part_o = reinterpret_cast<float*>(workspace);
+        a.part_o = workspace;
         a.part_ml = reinterpret_cast<float2*>(reinterpret_cast<char*>(workspace) + rows * kHeadDim * sizeof(float));
     }
     const int bh = c.batch * c.heads;

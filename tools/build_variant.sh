@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build a library variant from a kernel source file (A/B experiments; never shipped):
+#   tools/build_variant.sh <kernel.hip> <name> [extra hipcc flags...]  -> lib/exp/libmha_hd64_<name>.so
+set -e
+SRC=$(readlink -f "$1"); NAME=$2; shift 2
+cd "$(dirname "$0")/../lightglue-with-flashattentionv2-tensorrt_amd"
+mkdir -p lib/exp
+make -s lib/libmha_hd64.so
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans "$@" \
+      -I../include -Icsrc -c "$SRC" -o lib/exp/k_$NAME.o
+hipcc --offload-arch=gfx950 -shared -fPIC lib/exp/k_$NAME.o lib/obj/mha_hd64_plugin.o -o lib/exp/libmha_hd64_$NAME.so
+rm -f lib/exp/k_$NAME.o
+echo lib/exp/libmha_hd64_$NAME.so
