@@ -105,32 +105,57 @@ def event_durations_ms(torch, launch, n, stream):
     return [s.elapsed_time(e) for s, e in zip(starts, ends)]
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(seconds=10.0, nq=1024, nkv=1024):
     """Reference PyTorch CPU attention (lightglue_pytorch_no_plugin/lightglue.py:82-84, restated
-    in oracle/oracle.py) on this host, fp32, bounded sample of ~`seconds`."""
+    in oracle/oracle.py) on this host, fp32, bounded sample of ~`seconds` at the metric shape
+    with all torch threads; plus the SURVEY §8(d) grid (1 thread / all threads x 256^2 / 1024^2,
+    20 warm-ups then the median of >= 50 calls)."""
     import torch
 
     from lightglue_amd import synth
     from oracle import oracle
 
     threads = torch.get_num_threads()
-    qn, kn, vn = synth.qkv(2, nq, nkv)
-    q, k, v = (torch.from_numpy(x) for x in (qn, kn, vn))
-    for _ in range(3):
-        oracle.attention_torch(q, k, v)
-    n = 0
-    t0 = time.perf_counter()
-    times = []
-    while time.perf_counter() - t0 < seconds:
-        t1 = time.perf_counter()
-        oracle.attention_torch(q, k, v)
-        times.append(time.perf_counter() - t1)
-        n += 1
-    med = statistics.median(times)
-    return {"value": round(1.0 / med, 2), "unit": "calls/s", "cores": threads, "kind": "port",
-            "ms_per_call": round(med * 1e3, 3),
+
+    def median_ms(n_q, n_kv, nthreads, min_calls, budget_s):
+        torch.set_num_threads(nthreads)
+        qn, kn, vn = synth.qkv(2, n_q, n_kv)
+        q, k, v = (torch.from_numpy(x) for x in (qn, kn, vn))
+        for _ in range(20):
+            oracle.attention_torch(q, k, v)
+        times = []
+        t0 = time.perf_counter()
+        while len(times) < min_calls or time.perf_counter() - t0 < budget_s:
+            t1 = time.perf_counter()
+            oracle.attention_torch(q, k, v)
+            times.append(time.perf_counter() - t1)
+            if len(times) >= min_calls and time.perf_counter() - t0 > 4 * budget_s:
+                break
+        return statistics.median(times) * 1e3, len(times)
+
+    med, n = median_ms(nq, nkv, threads, 50, seconds)
+    grid = {}
+    for (a_, b_) in ((256, 256), (nq, nkv)):
+        for t in (1, threads):
+            ms, cnt = median_ms(a_, b_, t, 50, 0.5)
+            grid[f"{a_}x{b_}_{t}T_ms"] = round(ms, 4)
+    torch.set_num_threads(threads)
+    return {"value": round(1e3 / med, 2), "unit": "calls/s", "cores": threads, "kind": "port",
+            "ms_per_call": round(med, 3),
             "sample": f"{n} calls of 1x4x{nq}x{nkv} d=64 fp32, torch CPU matmul-softmax-matmul "
-                      f"(reference Attention.forward math), median per call, {threads} threads, ~{seconds:.0f}s"}
+                      f"(reference Attention.forward math), median per call, {threads} threads, ~{seconds:.0f}s",
+            "grid": grid, "cpu_model": _cpu_model(), "host_logical_cpus": os.cpu_count()}
 
 
 def load_traffic(tag):
@@ -171,6 +196,59 @@ def sweep(torch, lib, device, stream, nq, nkv):
                                   "main_us": round(t_main * 1e3, 2), "total_us": round(t_all * 1e3, 2),
                                   "main_tflops": round(fl / (t_main * 1e-3) / 1e12, 1)}), file=sys.stderr,
                       flush=True)
+
+
+def matcher_attention(torch, device, stream, rank, sizes=(512, 1024, 2048), layers=9, reps=20):
+    """BASELINE configs[3] (attention share): the 36 MHAHeadDim64 calls of a 9-layer LightGlue
+    matcher (per layer self0, self1, cross0->1, cross1->0; lightglue.py:216-226) at N0 = N1 = N,
+    captured in one graph, as 36 plugin enqueues vs 18 grouped launches (self pair + cross pair)."""
+    import lightglue_amd
+    from lightglue_amd import synth
+
+    res = {}
+    for n in sizes:
+        d = []
+        for i in range(4):
+            qn, kn, vn = synth.qkv(500 + 10 * rank + i + n, n, n)
+            d.append(tuple(torch.from_numpy(x).to(device).half().contiguous() for x in (qn, kn, vn)))
+        (q0, k0, v0), (q1, k1, v1) = d[0], d[1]
+        outs = [torch.empty_like(q0) for _ in range(4)]
+        calls = [(q0, k0, v0), (q1, k1, v1), (q0, k1, v1), (q1, k0, v0)]
+
+        def separate():
+            for _ in range(layers):
+                for c, o in zip(calls, outs):
+                    lightglue_amd.mha_hd64(*c, out=o)
+
+        def grouped():
+            for _ in range(layers):
+                lightglue_amd.mha_hd64_grouped(calls[:2], outs=outs[:2])
+                lightglue_amd.mha_hd64_grouped(calls[2:], outs=outs[2:])
+
+        times = {}
+        for name, fn in (("separate", separate), ("grouped", grouped)):
+            with torch.cuda.stream(stream):
+                fn()
+            stream.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream):
+                fn()
+            g.replay()
+            stream.synchronize()
+            s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_.record(stream)
+            with torch.cuda.stream(stream):
+                for _ in range(reps):
+                    g.replay()
+            e_.record(stream)
+            stream.synchronize()
+            times[name] = s_.elapsed_time(e_) / reps  # ms per matcher pass (36 calls)
+        fl = 4 * layers * call_flops(1, 4, n, n)
+        res[str(n)] = {"calls": 4 * layers, "separate_ms": round(times["separate"], 4),
+                       "grouped_ms": round(times["grouped"], 4),
+                       "grouped_tflops": round(fl / (times["grouped"] * 1e-3) / 1e12, 1),
+                       "grouped_frac": round(fl / (times["grouped"] * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4)}
+    return res
 
 
 def profile_driver(torch, args, device):
@@ -324,6 +402,8 @@ def main():
             "tflops": round(B * flops / (tb * 1e-3) / 1e12, 2),
             "frac": round(B * flops / (tb * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
         }
+
+        result["matcher_attention"] = matcher_attention(torch, device, stream, rank)
 
     if args.sweep and rank == 0:
         sweep(torch, lib, device, stream, nq, nkv)

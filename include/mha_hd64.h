@@ -159,6 +159,33 @@ int32_t mha_hd64_launch_fp32in_fp32out(const void* q, const void* k, const void*
  * this shape across workgroups (0 = the call never splits). */
 size_t mha_hd64_launch_workspace_bytes(int32_t batch, int32_t heads, int32_t nq, int32_t nkv);
 
+/* ---- grouped launcher ----
+ * Several independent calls of (possibly) different shapes in one launch. A LightGlue layer
+ * makes four attention calls whose inputs are all ready together: SelfBlock on image 0 and on
+ * image 1 (lightglue_pytorch_with_plugin/lightglue.py:137-152, Nq = Nkv = N0 and N1) and the
+ * two CrossBlock directions (lightglue.py:188-205, N0 x N1 and N1 x N0); the reference runs
+ * each as its own plugin enqueue (four kernel chains per layer, TransformerLayer :216-226).
+ * Up to 4 calls share one main-kernel launch (+ one combine launch when a call splits its
+ * keys); longer lists are chunked. All calls use one dtype pair:
+ *   in_type HALF  -> fp16 inputs; FLOAT -> fp32 inputs rounded to fp16 on load
+ *   out_type HALF -> fp16 output; FLOAT -> fp32 output
+ * Same per-call layout rules as the L0 launchers. Returns a status. */
+typedef struct mha_hd64_call {
+    const void* q;
+    const void* k;
+    const void* v;
+    void* o;
+    int32_t batch;
+    int32_t heads;
+    int32_t nq;
+    int32_t nkv;
+} mha_hd64_call_t;
+
+int32_t mha_hd64_launch_grouped(const mha_hd64_call_t* calls, int32_t n_calls, int32_t in_type,
+                                int32_t out_type, void* workspace, size_t ws_bytes, hipStream_t stream);
+/* Workspace bytes the grouped launcher can use (0 = no call of the group splits). */
+size_t mha_hd64_grouped_workspace_bytes(const mha_hd64_call_t* calls, int32_t n_calls);
+
 /* ---- diagnostics ---- */
 const char* mha_hd64_last_error(void);           /* thread-local message of the last failure   */
 void        mha_hd64_set_abort_on_error(int32_t enable); /* 1 = abort() like PLUGIN_ASSERT     */

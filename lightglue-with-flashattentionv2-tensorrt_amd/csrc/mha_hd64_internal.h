@@ -37,6 +37,26 @@ struct LaunchPlan {
     size_t ws_needed;     // workspace bytes the plan uses
 };
 
+// Up to kGroupCalls calls share one launch (grouped launcher); larger groups are chunked.
+constexpr int kGroupCalls = 4;
+
+// Plan of one launch carrying n <= kGroupCalls calls: one workgroup shape, per-call KV split,
+// per-call workspace offsets (split partials laid out call after call).
+struct GroupPlan {
+    int q_waves;
+    int kv_waves;
+    int splits[kGroupCalls];
+    int tiles_per_split[kGroupCalls];
+    size_t ws_offset[kGroupCalls];
+    size_t ws_needed;
+};
+GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_waves = 0, int force_kv_waves = 0,
+                     int force_splits = 0);
+hipError_t launch_group(const Call* calls, int n, InType in, OutType out, void* workspace, size_t ws_bytes,
+                        hipStream_t stream, int force_q_waves = 0, int force_kv_waves = 0, int force_splits = 0,
+                        int phase_mask = 3);
+size_t group_workspace_bytes(const Call* calls, int n);
+
 // Workgroup shapes compiled: (q_waves, kv_waves) in {(4,1), (2,2), (1,2), (4,2)}.
 LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves = 0, int force_kv_waves = 0,
                      int force_splits = 0);

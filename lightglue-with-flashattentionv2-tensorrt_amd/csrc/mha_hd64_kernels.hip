@@ -57,21 +57,40 @@ constexpr float kRescaleThr = 8.0f;                  // lazy-rescale threshold (
 constexpr int kTileKV = 64;                          // keys per LDS tile
 constexpr int kTileBytes = kTileKV * kHeadDim * 2;   // 8 KiB fp16 tile
 
-struct FwdArgs {
+// One call of a launch (a launch carries up to kMaxCalls independent calls of any shapes: the
+// grouped launcher runs self0+self1 or cross0->1+cross1->0 of a LightGlue layer as one launch).
+constexpr int kMaxCalls = kGroupCalls;
+struct CallArgs {
     const void* q;
     const void* k;
     const void* v;
     void* o;
-    void* part_o;    // [bh][splits][nq][64] O_s / l_s in TOut precision (splits > 1 only)
-    float2* part_ml; // [bh][splits][nq] (m in log2 units, l)
+    void* part_o;     // [bh][splits][nq][64] O_s / l_s in TOut precision (splits > 1 only)
+    float2* part_ml;  // [bh][splits][nq] (m in log2 units, l)
     int nq;
     int nkv;
     int splits;
     int tiles_per_split;
-    int qtiles;      // query blocks per (batch, head)
-    int bh;          // batch * heads
+    int qtiles;       // query blocks per (batch, head)
+    int bh;           // batch * heads
+    int block_begin;  // first block (in XCD-remapped order j) of this call
+    int pad_;
+};
+struct FwdArgs {
+    CallArgs c[kMaxCalls];
+    int n_calls;
+    int total_blocks;            // grid size (kept here so the first scalar-load round has it)
     unsigned long long* stamps;  // diagnostic builds only (MHA_STAMPS): 8 x u64 per workgroup
 };
+
+// Uniform (scalar) selection of call ci's arguments from the kernarg table (grouped launches).
+__device__ __forceinline__ CallArgs pick_call(const FwdArgs& a, int ci) {
+    CallArgs ca = a.c[0];
+#pragma unroll
+    for (int i = 1; i < kMaxCalls; ++i)
+        if (ci == i) ca = a.c[i];
+    return ca;
+}
 
 // LDS images (byte offsets inside one 8 KiB [64 rows][128 B] tile; chunk = 16 B = 8 halfs).
 // K is read row-wise by ds_read_b128 (lane = key row): XOR the chunk with (row>>1)&7
@@ -192,6 +211,21 @@ __device__ __forceinline__ void keep_live(const f16x8& x) { asm volatile("" ::"v
 #define MHA_PART_AUX 0  // cache policy bits of the split-partial stores
 #endif
 
+// Per-step phase clocks (diagnostic build -DMHA_STEPSTAMPS only): s_memtime at phase boundaries
+// of every full loop step, summed per wave, waited for only at the next step's barrier.
+#ifdef MHA_STEPSTAMPS
+#define TCLK(var)                                  \
+    do {                                           \
+        __builtin_amdgcn_sched_barrier(0);         \
+        var = __builtin_readcyclecounter();        \
+        __builtin_amdgcn_sched_barrier(0);         \
+    } while (0)
+#else
+#define TCLK(var) \
+    do {          \
+    } while (0)
+#endif
+
 constexpr float kMaskBias = -65504.f;  // fp16 lowest: a masked key's score, exp2 -> 0
 constexpr float kEmptyMax = -30000.f;  // tile max below this: every key of the tile was masked
 
@@ -232,7 +266,9 @@ __device__ __forceinline__ void bload8(Raw8<float>& r, __amdgpu_buffer_rsrc_t rs
 // (loaded into registers at the start of the iteration, written after phase B), one
 // barrier per iteration.
 // ----------------------------------------------------------------------------------------
-template <typename TIn, typename TOut, int QW, int KW>
+// MULTI = false: a launch of one call (plugin enqueue, L0 launchers) reads only c[0], so the
+// prologue's kernarg loads issue in one scalar round; MULTI = true: grouped launches.
+template <typename TIn, typename TOut, int QW, int KW, bool MULTI>
 __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a) {
     constexpr int NT = 64 * QW * KW;                // threads
     constexpr int BLOCK_M = 32 * QW;                // query rows per workgroup
@@ -254,33 +290,44 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     const int hh = lane >> 5;  // half-wave
     const int qw = wave % QW;
     const int kw = wave / QW;
-    const int nq = a.nq, nkv = a.nkv;
     // XCD-aware order (T1): the dispatcher deals consecutive blocks round-robin over the 8 XCDs;
     // renumber (bijectively, any count) so that the blocks sharing one XCD are consecutive in
-    // j = split + S*(qtile + qtiles*bh): the KV splits and neighbouring query blocks of one
-    // (batch, head) run on one XCD, read its K/V through one L2 and leave their split partials
-    // there for the combine kernel (which maps its blocks to the same XCD).
-    int qtile, bh, split;
+    // j = block_begin(call) + split + S*(qtile + qtiles*bh): the KV splits and neighbouring query
+    // blocks of one (batch, head) run on one XCD, read its K/V through one L2 and leave their
+    // split partials there for the combine kernel (which maps its blocks to the same XCD).
+    int qtile, bh, split, j;
     {
-        const int T = gridDim.x, L = blockIdx.x;
+        // branch-free (one basic block, so every kernarg load issues in one round):
+        // XCD x holds j in [x*q8 + min(x, r8), ...)
+        const int T = a.total_blocks, L = blockIdx.x;
         const int q8 = T >> 3, r8 = T & 7, xcd = L & 7;
-        const int j = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
-        split = j % a.splits;
-        const int g = j / a.splits;
-        qtile = g % a.qtiles;
-        bh = g / a.qtiles;
+        j = xcd * q8 + min(xcd, r8) + (L >> 3);
     }
-    const TIn* Qb = reinterpret_cast<const TIn*>(a.q) + (size_t)bh * nq * kHeadDim;
-    const TIn* Kb = reinterpret_cast<const TIn*>(a.k) + (size_t)bh * nkv * kHeadDim;
-    const TIn* Vb = reinterpret_cast<const TIn*>(a.v) + (size_t)bh * nkv * kHeadDim;
+    int ci = 0;
+    if constexpr (MULTI) {
+#pragma unroll
+        for (int i = 1; i < kMaxCalls; ++i) ci += (int)((i < a.n_calls) & (j >= a.c[i].block_begin));
+    }
+    const CallArgs ca = MULTI ? pick_call(a, ci) : a.c[0];
+    {
+        const int jl = j - ca.block_begin;
+        split = jl % ca.splits;
+        const int g = jl / ca.splits;
+        qtile = g % ca.qtiles;
+        bh = g / ca.qtiles;
+    }
+    const int nq = ca.nq, nkv = ca.nkv;
+    const TIn* Qb = reinterpret_cast<const TIn*>(ca.q) + (size_t)bh * nq * kHeadDim;
+    const TIn* Kb = reinterpret_cast<const TIn*>(ca.k) + (size_t)bh * nkv * kHeadDim;
+    const TIn* Vb = reinterpret_cast<const TIn*>(ca.v) + (size_t)bh * nkv * kHeadDim;
     const __amdgpu_buffer_rsrc_t q_rs = make_rsrc(Qb, (unsigned)nq * kHeadDim * SZ);
     const __amdgpu_buffer_rsrc_t k_rs = make_rsrc(Kb, (unsigned)nkv * kHeadDim * SZ);
     const __amdgpu_buffer_rsrc_t v_rs = make_rsrc(Vb, (unsigned)nkv * kHeadDim * SZ);
     const int q_row = qtile * BLOCK_M + qw * 32 + r;
 
     const int super_total = (nkv + SUPER - 1) / SUPER;
-    const int st_begin = split * a.tiles_per_split;
-    const int st_end = min(super_total, st_begin + a.tiles_per_split);
+    const int st_begin = split * ca.tiles_per_split;
+    const int st_end = min(super_total, st_begin + ca.tiles_per_split);
     const int n_iter = max(0, st_end - st_begin);
 
     // Staging: load i of this thread covers tile-tensor tt = i / PER (tile tt/2, K or V by tt&1),
@@ -419,6 +466,10 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     int st_cur = 0;
     auto next_stage = [](int st) { return st == NSTAGE - 1 ? 0 : st + 1; };
     // Step `it` writes super-tile it+2 from set `wr` and issues super-tile it+3 into set `is`.
+#ifdef MHA_STEPSTAMPS
+    unsigned long long ck[4] = {}, ck_prev[4] = {}, ck_sum[4] = {};
+    bool ck_first = true;
+#endif
     auto step = [&](int it, f32x16& c0, f32x16& c1, float mxc, f32x16& n0, f32x16& n1, float& mxn,
                     auto has_next_c, bool mask_next, Raw8<TIn>(&wr)[NLOAD], Raw8<TIn>(&is)[NLOAD],
                     bool may_issue) {
@@ -430,6 +481,7 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
         // descriptor returns zeros. A conditional load would make the compiler's vmcnt analysis
         // drain every load at the next LDS write (a one-step prefetch instead of two).
         if (!(MHA_ABL & ABL_NO_REFILL) && may_issue) issue(it + 3, is);
+        TCLK(ck[0]);
 
         // online-softmax decision for tile `it` (first tile: set the max exactly; later tiles:
         // move it only when some query's tile max exceeds it by > kRescaleThr)
@@ -483,16 +535,14 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
 #pragma unroll
             for (int i = 0; i < 10; ++i) {
                 qk_step(i, kf, ab0, ab1, n0, n1);
-                // LDS traffic spread over the MFMA phase instead of bursts at the step's ends:
-                // Vᵀ reads queue behind the K reads; the refill of stage it+2 (free since the
-                // last barrier) lands mid-phase.
+                // Vᵀ reads queue behind the K reads (phase A carries all fragment reads).
                 if (kEarlyV && i == 2) read_v();
-                if (i == 6 && !(MHA_ABL & ABL_NO_REFILL) && it + 2 < n_iter) write(st_fill, wr);
                 exp_at(3 * i);
                 exp_at(3 * i + 1);
                 exp_at(3 * i + 2);
                 __builtin_amdgcn_sched_barrier(0);
             }
+            TCLK(ck[1]);
             exp_at(30);
             exp_at(31);
         } else {
@@ -508,8 +558,11 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
             p[1][1][e] = (f16)c1[8 + e];
         }
 
-        // phase B: Oᵀ += Vᵀ·Pᵀ (it) and the row sums on the matrix pipe ‖ row max (it+1)
+        // phase B: Oᵀ += Vᵀ·Pᵀ (it) and the row sums on the matrix pipe ‖ row max (it+1) and the
+        // LDS refill of stage it+2 (free since the last barrier): phase A is LDS-read bound, so
+        // the refill's LDS writes go here, where the LDS is otherwise idle.
         if constexpr (!kEarlyV) read_v();
+        if (HAS_NEXT && !(MHA_ABL & ABL_NO_REFILL) && it + 2 < n_iter) write(st_fill, wr);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -531,7 +584,22 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
         }
 
         if (!HAS_NEXT && !(MHA_ABL & ABL_NO_REFILL) && it + 2 < n_iter) write(st_fill, wr);
+        TCLK(ck[2]);
+#ifdef MHA_STEPSTAMPS
+        if (HAS_NEXT) {  // previous full step's phases (its clocks have returned by now)
+            ck_sum[0] += ck_prev[1] - ck_prev[0];
+            ck_sum[1] += ck_prev[2] - ck_prev[1];
+            ck_sum[2] += ck_prev[3] - ck_prev[2];
+            ck_sum[3] += 1;
+        }
+#endif
         if (!(MHA_ABL & ABL_NO_BARRIER)) __syncthreads();
+        TCLK(ck[3]);
+#ifdef MHA_STEPSTAMPS
+        if (HAS_NEXT) {
+            for (int i = 0; i < 4; ++i) ck_prev[i] = ck[i];
+        }
+#endif
         st_cur = st_nxt;
     };
 
@@ -551,6 +619,12 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
         write(1, stgB);
         __syncthreads();
     }
+#ifndef MHA_PRIO
+#define MHA_PRIO 1
+#endif
+    // Two waves per SIMD: the second-dispatched half loses every age-ordered issue arbitration
+    // and arrives last at each barrier; static priority for that half evens the two out.
+    if (MHA_PRIO && NT == 512 && wave >= 4) __builtin_amdgcn_s_setprio(1);
     int it = 0;
     // Steady state: tiles it+1 and it+2 exist and neither is the (possibly partial) last one.
     for (; it + 3 < n_iter; it += 2) {
@@ -601,10 +675,10 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     // buffer stores through per-head descriptors (cache policy MHA_ST_AUX / MHA_PART_AUX).
     const int q_base = qtile * BLOCK_M;
     const __amdgpu_buffer_rsrc_t o_rs =
-        make_rsrc(reinterpret_cast<TOut*>(a.o) + (size_t)bh * nq * kHeadDim, (unsigned)(nq * kHeadDim * sizeof(TOut)));
+        make_rsrc(reinterpret_cast<TOut*>(ca.o) + (size_t)bh * nq * kHeadDim, (unsigned)(nq * kHeadDim * sizeof(TOut)));
     const __amdgpu_buffer_rsrc_t po_rs =
-        make_rsrc(reinterpret_cast<TOut*>(a.part_o) + (size_t)bh * a.splits * nq * kHeadDim,
-                  (unsigned)(a.splits * nq * kHeadDim * sizeof(TOut)));
+        make_rsrc(reinterpret_cast<TOut*>(ca.part_o) + (size_t)bh * ca.splits * nq * kHeadDim,
+                  (unsigned)(ca.splits * nq * kHeadDim * sizeof(TOut)));
 #pragma unroll
     for (int pass = 0; pass < (BLOCK_M * 8) / NT; ++pass) {
         const int idx = pass * NT + tid;
@@ -629,7 +703,7 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
             acc1 += w * *reinterpret_cast<const f32x4*>(src + 4);
         }
         if (q < nq && !(MHA_ABL & ABL_NO_STORE)) {
-            if (a.splits == 1) {
+            if (ca.splits == 1) {
                 const float inv = 1.f / L;
                 store8<TOut, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c8) * sizeof(TOut)), acc0 * inv, acc1 * inv);
             } else {
@@ -639,11 +713,19 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
                 const float inv = (L > 0.f) ? 1.f / L : 0.f;
                 store8<TOut, MHA_PART_AUX>(po_rs, prow * (unsigned)(kHeadDim * sizeof(TOut)) + c8 * (unsigned)sizeof(TOut),
                                            acc0 * inv, acc1 * inv);
-                if (c8 == 0) a.part_ml[((size_t)bh * a.splits) * nq + prow] = make_float2(M, L);
+                if (c8 == 0) ca.part_ml[((size_t)bh * ca.splits) * nq + prow] = make_float2(M, L);
             }
         }
     }
     STAMP(4);
+#ifdef MHA_STEPSTAMPS
+    if (lane == 0) {
+        unsigned long long* dst = a.stamps + (1 << 16) + ((size_t)blockIdx.x * 8 + wave) * 4;
+        // the first accumulated step has zero deltas (ck_prev unset): subtract it out on the host
+        for (int i = 0; i < 4; ++i) dst[i] = ck_sum[i];
+    }
+    (void)ck_first;
+#endif
 }
 
 // ----------------------------------------------------------------------------------------
@@ -654,23 +736,29 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
 // ----------------------------------------------------------------------------------------
 constexpr int kMaxSplits = 16;
 
-struct CombineArgs {
+struct CombineCall {
     const void* part_o;
     const float2* part_ml;
     void* out;
     int nq;
     int splits;
-    int qtiles;      // query blocks per (batch, head) of the main kernel
-    int block_m;     // rows per query block
-    int groups;      // qtiles * bh
-    int main_blocks; // grid of the main kernel (groups * splits)
-    int per_xcd;     // combine blocks per XCD
+    int qtiles;       // query blocks per (batch, head) of the main kernel
+    int pad_;
 };
-
-__device__ __forceinline__ int xcd_j_begin(int T, int x) {
-    const int q8 = T >> 3, r8 = T & 7;
-    return x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
-}
+// Block b of the combine grid serves XCD x = b % 8 (k = b / 8): blocks k in
+// [kbeg[x][i], kbeg[x][i+1]) serve call i, starting at query group gbeg[x][i] (the first group
+// whose first split block ran on XCD x). A block is 16 rows of one query group (block_m is a
+// multiple of 16), so the call, the group and its (batch*head, query block) are block-uniform.
+struct CombineArgs {
+    CombineCall c[kMaxCalls];
+    int kbeg[8][kMaxCalls + 1];
+    int gbeg[8][kMaxCalls];
+    int n_calls;
+    int block_m_log2;  // rows per query block = 1 << block_m_log2
+    int per_xcd;       // combine blocks per XCD
+    int main_blocks;   // single-call form: grid of the main kernel
+    int groups0;       // single-call form: query groups of call 0
+};
 
 template <typename T>
 __device__ __forceinline__ f32x4 load4f(const T* p) {
@@ -682,88 +770,105 @@ __device__ __forceinline__ f32x4 load4f(const T* p) {
     }
 }
 
-template <typename TOut>
+// MULTI = false (one call): the XCD's first group is computed from the main grid in scalar
+// arithmetic (no dependent kernarg table lookups); MULTI = true reads the per-XCD table.
+template <typename TOut, bool MULTI>
 __global__ __launch_bounds__(256) void mha_hd64_combine_kernel(CombineArgs c) {
     const int x = blockIdx.x & 7, k = blockIdx.x >> 3;
-    // Groups (query blocks) whose first split block the main kernel ran on XCD x.
-    const int jlo = xcd_j_begin(c.main_blocks, x), jhi = xcd_j_begin(c.main_blocks, x + 1);
-    const int glo = (jlo + c.splits - 1) / c.splits, ghi = min(c.groups, (jhi + c.splits - 1) / c.splits);
-    const int local = k * 256 + threadIdx.x;
-    const int lrow = local >> 4;
-    const int g = glo + lrow / c.block_m;
-    if (g >= ghi) return;
-    const int chunk = local & 15;
-    const int bh = g / c.qtiles, qt = g - bh * c.qtiles;
-    const int q = qt * c.block_m + lrow % c.block_m;
-    if (q >= c.nq) return;
-    const size_t base = (size_t)bh * c.splits * c.nq + q;
-    const TOut* po = reinterpret_cast<const TOut*>(c.part_o);
+    CombineCall cc = c.c[0];
+    int kb = 0, gb;
+    if constexpr (MULTI) {
+        int ci = -1;
+#pragma unroll
+        for (int i = 0; i < kMaxCalls; ++i)
+            if (i < c.n_calls && k >= c.kbeg[x][i] && k < c.kbeg[x][i + 1]) ci = i;
+        if (ci < 0) return;
+        kb = c.kbeg[x][0];
+        gb = c.gbeg[x][0];
+#pragma unroll
+        for (int i = 1; i < kMaxCalls; ++i)
+            if (ci == i) {
+                cc = c.c[i];
+                kb = c.kbeg[x][i];
+                gb = c.gbeg[x][i];
+            }
+    } else {
+        const int T = c.main_blocks, q8 = T >> 3, r8 = T & 7;
+        const int jlo = x * q8 + min(x, r8), jhi = (x + 1) * q8 + min(x + 1, r8);
+        const int groups = c.groups0;
+        const int glo = min(groups, (jlo + cc.splits - 1) / cc.splits);
+        const int ghi = min(groups, (jhi + cc.splits - 1) / cc.splits);
+        if (k >= ((ghi - glo) << c.block_m_log2) / 16) return;
+        gb = glo;
+    }
+    const int row0 = (k - kb) * 16;                       // first row of this block in the segment
+    const int g = gb + (row0 >> c.block_m_log2);          // block-uniform query group
+    const int bh = g / cc.qtiles, qt = g - bh * cc.qtiles;
+    const int q = (qt << c.block_m_log2) + (row0 & ((1 << c.block_m_log2) - 1)) + ((int)threadIdx.x >> 4);
+    if (q >= cc.nq) return;
+    const int chunk = threadIdx.x & 15;
+    const size_t base = (size_t)bh * cc.splits * cc.nq + q;
+    const TOut* po = reinterpret_cast<const TOut*>(cc.part_o);
     float2 ml[kMaxSplits];
     f32x4 v[kMaxSplits];
 #pragma unroll
     for (int s = 0; s < kMaxSplits; ++s) {
-        if (s < c.splits) {
-            const size_t pr = base + (size_t)s * c.nq;
-            ml[s] = c.part_ml[pr];
+        if (s < cc.splits) {
+            const size_t pr = base + (size_t)s * cc.nq;
+            ml[s] = cc.part_ml[pr];
             v[s] = load4f<TOut>(po + pr * kHeadDim + chunk * 4);
         }
     }
     float M = -INFINITY;
 #pragma unroll
     for (int s = 0; s < kMaxSplits; ++s)
-        if (s < c.splits) M = fmaxf(M, ml[s].x);
+        if (s < cc.splits) M = fmaxf(M, ml[s].x);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     float L = 0.f;
 #pragma unroll
     for (int s = 0; s < kMaxSplits; ++s) {
-        if (s < c.splits) {
+        if (s < cc.splits) {
             const float w = (ml[s].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[s].x - M) * ml[s].y;
             L += w;
             acc += w * v[s];
         }
     }
     const float inv = 1.f / L;
-    TOut* out = reinterpret_cast<TOut*>(c.out) + ((size_t)bh * c.nq + q) * kHeadDim + chunk * 4;
+    TOut* out = reinterpret_cast<TOut*>(cc.out) + ((size_t)bh * cc.nq + q) * kHeadDim + chunk * 4;
     store4<TOut>(out, acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
 }
 
-template <typename TIn, typename TOut, int QW, int KW>
-hipError_t launch_fwd(const FwdArgs& a, int bh, hipStream_t stream) {
-    FwdArgs b = a;
-    b.qtiles = (a.nq + 32 * QW - 1) / (32 * QW);
-    b.bh = bh;
-    const dim3 grid(b.qtiles * bh * a.splits);
-    hipLaunchKernelGGL((mha_hd64_fwd_kernel<TIn, TOut, QW, KW>), grid, dim3(64 * QW * KW), 0, stream, b);
+template <typename TIn, typename TOut, int QW, int KW, bool MULTI>
+hipError_t launch_fwd(const FwdArgs& a, int grid, hipStream_t stream) {
+    hipLaunchKernelGGL((mha_hd64_fwd_kernel<TIn, TOut, QW, KW, MULTI>), dim3(grid), dim3(64 * QW * KW), 0, stream, a);
     return hipGetLastError();
 }
 
+// Grouped launches (several calls) exist for the two shapes the planner picks on its own.
 template <typename TIn, typename TOut>
-hipError_t launch_fwd_shape(const FwdArgs& a, int bh, int qw, int kw, hipStream_t stream) {
+hipError_t launch_fwd_shape(const FwdArgs& a, int grid, int qw, int kw, hipStream_t stream) {
+    if (a.n_calls > 1) {
+        switch (qw * 8 + kw) {
+            case 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, true>(a, grid, stream);
+            case 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2, true>(a, grid, stream);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (qw * 8 + kw) {
-        case 4 * 8 + 1: return launch_fwd<TIn, TOut, 4, 1>(a, bh, stream);
-        case 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2>(a, bh, stream);
-        case 1 * 8 + 2: return launch_fwd<TIn, TOut, 1, 2>(a, bh, stream);
-        case 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2>(a, bh, stream);
+        case 4 * 8 + 1: return launch_fwd<TIn, TOut, 4, 1, false>(a, grid, stream);
+        case 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, false>(a, grid, stream);
+        case 1 * 8 + 2: return launch_fwd<TIn, TOut, 1, 2, false>(a, grid, stream);
+        case 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2, false>(a, grid, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <typename TOut>
-hipError_t launch_combine(const FwdArgs& a, int bh, int qw, hipStream_t stream) {
-    CombineArgs c{};
-    c.part_o = a.part_o;
-    c.part_ml = a.part_ml;
-    c.out = a.o;
-    c.nq = a.nq;
-    c.splits = a.splits;
-    c.block_m = 32 * qw;
-    c.qtiles = (a.nq + c.block_m - 1) / c.block_m;
-    c.groups = c.qtiles * bh;
-    c.main_blocks = c.groups * a.splits;
-    // Rows per XCD: at most ceil(groups / 8) + 1 groups (the split ranges may straddle).
-    const int max_groups_per_xcd = (c.groups + 7) / 8 + 1;
-    c.per_xcd = (max_groups_per_xcd * c.block_m * 16 + 255) / 256;
-    hipLaunchKernelGGL((mha_hd64_combine_kernel<TOut>), dim3(8 * c.per_xcd), dim3(256), 0, stream, c);
+hipError_t launch_combine(const CombineArgs& c, hipStream_t stream) {
+    if (c.n_calls > 1)
+        hipLaunchKernelGGL((mha_hd64_combine_kernel<TOut, true>), dim3(8 * c.per_xcd), dim3(256), 0, stream, c);
+    else
+        hipLaunchKernelGGL((mha_hd64_combine_kernel<TOut, false>), dim3(8 * c.per_xcd), dim3(256), 0, stream, c);
     return hipGetLastError();
 }
 
@@ -773,6 +878,8 @@ bool valid_shape(int qw, int kw) {
 
 unsigned long long* g_stamps = nullptr;  // diagnostic builds (MHA_STAMPS) only
 
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 }  // namespace
 
 void set_stamp_buffer(void* p) { g_stamps = reinterpret_cast<unsigned long long*>(p); }
@@ -781,14 +888,17 @@ size_t split_workspace_bytes(const Call& c, int splits) {
     if (splits <= 1) return 0;
     const size_t rows = (size_t)c.batch * c.heads * splits * c.nq;
     const size_t o_bytes = rows * kHeadDim * sizeof(float);  // fp32 bound (fp16 partials use half)
-    return o_bytes + rows * sizeof(float2);
+    return align256(o_bytes) + align256(rows * sizeof(float2));
 }
 
-LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves, int force_kv_waves, int force_splits) {
-    const int bh = c.batch * c.heads;
+GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_waves, int force_kv_waves,
+                     int force_splits) {
+    GroupPlan p{};
     int qw = force_q_waves, kw = force_kv_waves;
     if (!valid_shape(qw, kw)) {
-        if (bh * ((c.nq + 127) / 128) >= 256) {
+        long blocks128 = 0;
+        for (int i = 0; i < n; ++i) blocks128 += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 127) / 128);
+        if (blocks128 >= 256) {
             qw = 4;  // enough 128-row query blocks to fill the chip: 8 waves, no cross-WG split
             kw = 2;
         } else {
@@ -796,62 +906,156 @@ LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves, int forc
             kw = 2;
         }
     }
-    const int qtiles = (c.nq + 32 * qw - 1) / (32 * qw);
-    const int super_total = (c.nkv + 64 * kw - 1) / (64 * kw);
-    int want = force_splits > 0 ? force_splits : (256 + qtiles * bh - 1) / (qtiles * bh);
-    want = std::max(1, std::min(std::min(want, super_total), kMaxSplits));
-    LaunchPlan p{};
     p.q_waves = qw;
     p.kv_waves = kw;
+    long groups = 0;
+    for (int i = 0; i < n; ++i)
+        groups += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 32 * qw - 1) / (32 * qw));
+    int want = force_splits > 0 ? force_splits : (int)std::max(1L, (256 + groups - 1) / std::max(1L, groups));
+    want = std::max(1, std::min(want, kMaxSplits));
     for (;;) {
-        p.tiles_per_split = (super_total + want - 1) / want;
-        p.splits = (super_total + p.tiles_per_split - 1) / p.tiles_per_split;
-        p.ws_needed = split_workspace_bytes(c, p.splits);
-        if (p.splits <= 1 || p.ws_needed <= ws_bytes) break;
-        want = p.splits - 1;
-    }
-    if (p.splits <= 1) {
-        p.splits = 1;
-        p.tiles_per_split = std::max(1, super_total);
-        p.ws_needed = 0;
+        size_t off = 0;
+        for (int i = 0; i < n; ++i) {
+            const int super_total = std::max(1, (calls[i].nkv + 64 * kw - 1) / (64 * kw));
+            const int w = std::min(want, super_total);
+            p.tiles_per_split[i] = (super_total + w - 1) / w;
+            p.splits[i] = (super_total + p.tiles_per_split[i] - 1) / p.tiles_per_split[i];
+            p.ws_offset[i] = off;
+            off += split_workspace_bytes(calls[i], p.splits[i]);
+        }
+        p.ws_needed = off;
+        if (want <= 1 || off <= ws_bytes) break;
+        --want;
     }
     return p;
+}
+
+LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves, int force_kv_waves, int force_splits) {
+    const GroupPlan g = plan_group(&c, 1, ws_bytes, force_q_waves, force_kv_waves, force_splits);
+    LaunchPlan p{};
+    p.q_waves = g.q_waves;
+    p.kv_waves = g.kv_waves;
+    p.splits = g.splits[0];
+    p.tiles_per_split = g.tiles_per_split[0];
+    p.ws_needed = g.ws_needed;
+    return p;
+}
+
+static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutType out, void* workspace,
+                                     size_t ws_bytes, hipStream_t stream, int force_q_waves, int force_kv_waves,
+                                     int force_splits, int phase_mask) {
+    const GroupPlan p = plan_group(calls, n, workspace ? ws_bytes : 0, force_q_waves, force_kv_waves, force_splits);
+    FwdArgs a{};
+    CombineArgs cb{};
+    a.stamps = g_stamps;
+    int blocks = 0, n_live = 0;
+    bool any_split = false;
+    for (int i = 0; i < n; ++i) {
+        const Call& c = calls[i];
+        if (c.nq <= 0 || c.batch <= 0 || c.heads <= 0) continue;  // nothing to compute
+        CallArgs& ca = a.c[n_live];
+        ca.q = c.q;
+        ca.k = c.k;
+        ca.v = c.v;
+        ca.o = c.o;
+        ca.nq = c.nq;
+        ca.nkv = c.nkv;
+        ca.splits = p.splits[i];
+        ca.tiles_per_split = p.tiles_per_split[i];
+        ca.bh = c.batch * c.heads;
+        ca.qtiles = (c.nq + 32 * p.q_waves - 1) / (32 * p.q_waves);
+        ca.block_begin = blocks;
+        if (ca.splits > 1) {
+            const size_t rows = (size_t)ca.bh * ca.splits * c.nq;
+            char* base = reinterpret_cast<char*>(workspace) + p.ws_offset[i];
+            ca.part_o = base;
+            ca.part_ml = reinterpret_cast<float2*>(base + align256(rows * kHeadDim * sizeof(float)));
+            any_split = true;
+        }
+        CombineCall& cc = cb.c[n_live];
+        cc.part_o = ca.part_o;
+        cc.part_ml = ca.part_ml;
+        cc.out = c.o;
+        cc.nq = c.nq;
+        cc.splits = ca.splits;
+        cc.qtiles = ca.qtiles;
+        blocks += ca.qtiles * ca.bh * ca.splits;
+        ++n_live;
+    }
+    if (n_live == 0) return hipSuccess;
+    a.n_calls = n_live;
+    a.total_blocks = blocks;
+    hipError_t e = hipSuccess;
+    if (phase_mask & 1) {
+        if (in == InType::F16) {
+            e = (out == OutType::F16) ? launch_fwd_shape<f16, f16>(a, blocks, p.q_waves, p.kv_waves, stream)
+                                      : launch_fwd_shape<f16, float>(a, blocks, p.q_waves, p.kv_waves, stream);
+        } else {
+            e = (out == OutType::F16) ? launch_fwd_shape<float, f16>(a, blocks, p.q_waves, p.kv_waves, stream)
+                                      : launch_fwd_shape<float, float>(a, blocks, p.q_waves, p.kv_waves, stream);
+        }
+    }
+    if (e != hipSuccess || !any_split || !(phase_mask & 2)) return e;
+    // Combine grid: for every XCD x, the groups (of calls that split) whose first split block
+    // ran on x (same bijective order as the main kernel), 16 rows per block.
+    cb.n_calls = n_live;
+    const int block_m = 32 * p.q_waves;
+    cb.block_m_log2 = block_m == 32 ? 5 : (block_m == 64 ? 6 : 7);
+    auto xb = [&](int xx) {
+        const int q8 = blocks >> 3, r8 = blocks & 7;
+        return xx < r8 ? xx * (q8 + 1) : r8 * (q8 + 1) + (xx - r8) * q8;
+    };
+    auto fg = [](int j, int b0, int S) { return j <= b0 ? 0 : (j - b0 + S - 1) / S; };
+    int per_xcd = 0;
+    for (int x = 0; x < 8; ++x) {
+        const int jlo = xb(x), jhi = xb(x + 1);
+        int kk = 0;
+        for (int i = 0; i < n_live; ++i) {
+            cb.kbeg[x][i] = kk;
+            const CallArgs& ca = a.c[i];
+            if (ca.splits <= 1) {
+                cb.gbeg[x][i] = 0;
+                continue;
+            }
+            const int groups = ca.qtiles * ca.bh;
+            const int glo = std::min(groups, fg(jlo, ca.block_begin, ca.splits));
+            const int ghi = std::min(groups, fg(jhi, ca.block_begin, ca.splits));
+            cb.gbeg[x][i] = glo;
+            kk += (ghi - glo) * block_m / 16;
+        }
+        for (int i = n_live; i <= kMaxCalls; ++i) cb.kbeg[x][i] = kk;
+        per_xcd = std::max(per_xcd, kk);
+    }
+    cb.per_xcd = std::max(1, per_xcd);
+    cb.main_blocks = blocks;
+    cb.groups0 = a.c[0].qtiles * a.c[0].bh;
+    return (out == OutType::F16) ? launch_combine<f16>(cb, stream) : launch_combine<float>(cb, stream);
+}
+
+hipError_t launch_group(const Call* calls, int n, InType in, OutType out, void* workspace, size_t ws_bytes,
+                        hipStream_t stream, int force_q_waves, int force_kv_waves, int force_splits,
+                        int phase_mask) {
+    // Chunks of kMaxCalls calls share one launch; each chunk reuses the workspace (stream order).
+    for (int i = 0; i < n; i += kMaxCalls) {
+        const hipError_t e = launch_group_chunk(calls + i, std::min(kMaxCalls, n - i), in, out, workspace, ws_bytes,
+                                                stream, force_q_waves, force_kv_waves, force_splits, phase_mask);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+size_t group_workspace_bytes(const Call* calls, int n) {
+    size_t need = 0;
+    for (int i = 0; i < n; i += kMaxCalls)
+        need = std::max(need, plan_group(calls + i, std::min(kMaxCalls, n - i), (size_t)-1).ws_needed);
+    return need;
 }
 
 hipError_t launch_attention(const Call& c, InType in, OutType out, void* workspace, size_t ws_bytes,
                             hipStream_t stream, int force_q_waves, int force_kv_waves, int force_splits,
                             int phase_mask) {
-    if (c.nq <= 0 || c.batch <= 0 || c.heads <= 0) return hipSuccess;  // nothing to compute
-    const LaunchPlan p = plan_call(c, workspace ? ws_bytes : 0, force_q_waves, force_kv_waves, force_splits);
-    FwdArgs a{};
-    a.q = c.q;
-    a.k = c.k;
-    a.v = c.v;
-    a.o = c.o;
-    a.nq = c.nq;
-    a.nkv = c.nkv;
-    a.splits = p.splits;
-    a.tiles_per_split = p.tiles_per_split;
-    a.stamps = g_stamps;
-    if (p.splits > 1) {
-        const size_t rows = (size_t)c.batch * c.heads * p.splits * c.nq;
-        a.part_o = workspace;
-        a.part_ml = reinterpret_cast<float2*>(reinterpret_cast<char*>(workspace) + rows * kHeadDim * sizeof(float));
-    }
-    const int bh = c.batch * c.heads;
-    hipError_t e = hipSuccess;
-    if (phase_mask & 1) {
-        if (in == InType::F16) {
-            e = (out == OutType::F16) ? launch_fwd_shape<f16, f16>(a, bh, p.q_waves, p.kv_waves, stream)
-                                      : launch_fwd_shape<f16, float>(a, bh, p.q_waves, p.kv_waves, stream);
-        } else {
-            e = (out == OutType::F16) ? launch_fwd_shape<float, f16>(a, bh, p.q_waves, p.kv_waves, stream)
-                                      : launch_fwd_shape<float, float>(a, bh, p.q_waves, p.kv_waves, stream);
-        }
-    }
-    if (e != hipSuccess || p.splits == 1 || !(phase_mask & 2)) return e;
-    return (out == OutType::F16) ? launch_combine<f16>(a, bh, p.q_waves, stream)
-                                 : launch_combine<float>(a, bh, p.q_waves, stream);
+    return launch_group_chunk(&c, 1, in, out, workspace, ws_bytes, stream, force_q_waves, force_kv_waves,
+                              force_splits, phase_mask);
 }
 
 }  // namespace mha_hd64

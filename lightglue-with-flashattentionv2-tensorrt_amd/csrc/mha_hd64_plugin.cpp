@@ -23,6 +23,7 @@
 #include <exception>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "mha_hd64.h"
 #include "mha_hd64_internal.h"
@@ -310,6 +311,43 @@ size_t mha_hd64_launch_workspace_bytes(int32_t batch, int32_t heads, int32_t nq,
     const mha_hd64::Call c{nullptr, nullptr, nullptr, nullptr, batch, heads, nq, nkv};
     // Plan with an unbounded workspace to learn what the preferred split needs.
     return mha_hd64::plan_call(c, (size_t)-1).ws_needed;
+}
+
+// ---- grouped launcher ----
+static int32_t to_calls(const mha_hd64_call_t* calls, int32_t n, std::vector<mha_hd64::Call>& out) {
+    MHA_CHECK(n >= 0 && (n == 0 || calls != nullptr));
+    out.clear();
+    for (int32_t i = 0; i < n; ++i) {
+        const mha_hd64_call_t& c = calls[i];
+        MHA_CHECK(c.batch >= 0 && c.heads >= 0 && c.nq >= 0 && c.nkv >= 0);
+        if (c.batch == 0 || c.heads == 0 || c.nq == 0) continue;
+        MHA_CHECK(c.nkv >= 1);
+        MHA_CHECK(c.q != nullptr && c.k != nullptr && c.v != nullptr && c.o != nullptr);
+        MHA_CHECK(((uintptr_t)c.q | (uintptr_t)c.k | (uintptr_t)c.v | (uintptr_t)c.o) % 16 == 0);
+        out.push_back(mha_hd64::Call{c.q, c.k, c.v, c.o, c.batch, c.heads, c.nq, c.nkv});
+    }
+    return MHA_HD64_STATUS_SUCCESS;
+}
+
+int32_t mha_hd64_launch_grouped(const mha_hd64_call_t* calls, int32_t n_calls, int32_t in_type, int32_t out_type,
+                                void* workspace, size_t ws_bytes, hipStream_t stream) {
+    MHA_CHECK(in_type == MHA_HD64_DT_HALF || in_type == MHA_HD64_DT_FLOAT);
+    MHA_CHECK(out_type == MHA_HD64_DT_HALF || out_type == MHA_HD64_DT_FLOAT);
+    std::vector<mha_hd64::Call> v;
+    const int32_t st = to_calls(calls, n_calls, v);
+    if (st != MHA_HD64_STATUS_SUCCESS || v.empty()) return st;
+    return launch_status(
+        mha_hd64::launch_group(v.data(), (int)v.size(),
+                               in_type == MHA_HD64_DT_HALF ? mha_hd64::InType::F16 : mha_hd64::InType::F32,
+                               out_type == MHA_HD64_DT_HALF ? mha_hd64::OutType::F16 : mha_hd64::OutType::F32,
+                               workspace, workspace ? ws_bytes : 0, stream),
+        __FILE__, __LINE__);
+}
+
+size_t mha_hd64_grouped_workspace_bytes(const mha_hd64_call_t* calls, int32_t n_calls) {
+    std::vector<mha_hd64::Call> v;
+    if (to_calls(calls, n_calls, v) != MHA_HD64_STATUS_SUCCESS || v.empty()) return 0;
+    return mha_hd64::group_workspace_bytes(v.data(), (int)v.size());
 }
 
 // ---- diagnostics ----

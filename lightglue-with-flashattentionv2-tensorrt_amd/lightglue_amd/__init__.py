@@ -11,6 +11,7 @@ from .plugin import (  # noqa: F401
     PluginError,
     mha_hd64,
     mha_hd64_batched,
+    mha_hd64_grouped,
 )
 
 __all__ = [
@@ -21,6 +22,7 @@ __all__ = [
     "PluginError",
     "mha_hd64",
     "mha_hd64_batched",
+    "mha_hd64_grouped",
     "load_library",
     "LIB_PATH",
 ]

@@ -70,6 +70,13 @@ class DynamicTensorDesc(ctypes.Structure):
         return t
 
 
+class CallDesc(ctypes.Structure):
+    """Mirrors mha_hd64_call_t (one call of a grouped launch)."""
+    _fields_ = [("q", ctypes.c_void_p), ("k", ctypes.c_void_p), ("v", ctypes.c_void_p), ("o", ctypes.c_void_p),
+                ("batch", ctypes.c_int32), ("heads", ctypes.c_int32), ("nq", ctypes.c_int32),
+                ("nkv", ctypes.c_int32)]
+
+
 # Every symbol include/mha_hd64.h declares, with its ctypes signature.
 _P = ctypes.c_void_p
 _I = ctypes.c_int32
@@ -105,6 +112,8 @@ SIGNATURES = {
     "mha_hd64_launch_fp16in_fp32out": ([_P, _P, _P, _P, _I, _I, _I, _I, _P, _S, _P], _I),
     "mha_hd64_launch_fp32in_fp32out": ([_P, _P, _P, _P, _I, _I, _I, _I, _P, _S, _P], _I),
     "mha_hd64_launch_workspace_bytes": ([_I, _I, _I, _I], _S),
+    "mha_hd64_launch_grouped": ([ctypes.POINTER(CallDesc), _I, _I, _I, _P, _S, _P], _I),
+    "mha_hd64_grouped_workspace_bytes": ([ctypes.POINTER(CallDesc), _I], _S),
     "mha_hd64_last_error": ([], _C),
     "mha_hd64_set_abort_on_error": ([_I], None),
     "mha_hd64_build_info": ([], _C),

@@ -287,6 +287,45 @@ def mha_hd64_batched(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor
     return out
 
 
+_DT = {torch.float16: _lib.DT_HALF, torch.float32: _lib.DT_FLOAT}
+
+
+def mha_hd64_grouped(calls, out_dtype=None, outs=None):
+    """Grouped launcher: several independent calls [(q, k, v), ...] of possibly different shapes
+    ([B, H, Nq_i, 64] / [B, H, Nkv_i, 64]) in one launch (up to 4 per launch, chunked beyond).
+
+    The four attention calls of a LightGlue layer (self0, self1, cross0->1, cross1->0;
+    lightglue_pytorch_with_plugin/lightglue.py:137-152, 188-205) run as two such launches."""
+    calls = list(calls)
+    if not calls:
+        return []
+    in_dtype = calls[0][0].dtype
+    out_dtype = out_dtype or in_dtype
+    if in_dtype not in _DT or out_dtype not in _DT:
+        raise PluginError(f"unsupported dtypes {in_dtype} -> {out_dtype}")
+    if outs is None:
+        outs = [torch.empty(q.shape, dtype=out_dtype, device=q.device) for q, _, _ in calls]
+    descs = (_lib.CallDesc * len(calls))()
+    for i, ((q, k, v), o) in enumerate(zip(calls, outs)):
+        _require_gpu(q, k, v, o)
+        for t in (q, k, v):
+            if not t.is_contiguous() or t.dim() != 4 or t.shape[-1] != 64 or t.dtype != in_dtype:
+                raise PluginError("expected contiguous [B, H, N, 64] tensors of one dtype")
+        if k.shape != v.shape or k.shape[:2] != q.shape[:2] or o.shape != q.shape or o.dtype != out_dtype:
+            raise PluginError("shape mismatch in grouped call")
+        descs[i] = _lib.CallDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), q.shape[0], q.shape[1],
+                                 q.shape[2], k.shape[2])
+    lib = _lib.load()
+    device = calls[0][0].device
+    stream = torch.cuda.current_stream(device).cuda_stream
+    nbytes = lib.mha_hd64_grouped_workspace_bytes(descs, len(calls))
+    ws = _workspace(device, stream, nbytes) if nbytes else None
+    status = lib.mha_hd64_launch_grouped(descs, len(calls), _DT[in_dtype], _DT[out_dtype],
+                                         ws.data_ptr() if ws is not None else None, nbytes, stream)
+    _check(status, "mha_hd64_launch_grouped")
+    return outs
+
+
 class MHAHeadDim64(torch.autograd.Function):
     """lightglue_pytorch_with_plugin/lightglue.py:16-46, forward on the MI355X kernel."""
 

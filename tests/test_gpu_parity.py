@@ -266,3 +266,70 @@ def test_streams_with_separate_workspaces(dev):
     torch.cuda.synchronize()
     for o in outs:
         assert torch.equal(o, ref)
+
+
+# ---- grouped launcher: several calls of different shapes per launch ----
+def _group_inputs(shapes, seed, dtype=np.float16):
+    from lightglue_amd import synth
+
+    out = []
+    for i, (b, nq, nkv) in enumerate(shapes):
+        qn, kn, vn = synth.qkv(seed + 17 * i, nq, nkv, batch=b)
+        out.append(tuple(synth.round_f16(x) for x in (qn, kn, vn)) if dtype == np.float16 else (qn, kn, vn))
+    return out
+
+
+def test_grouped_lightglue_layer(dev, oracle_mod):
+    """One LightGlue layer's four calls (self0, self1, cross0->1, cross1->0; lightglue.py:137-152,
+    188-205) as two grouped launches and as one, each output against the oracle."""
+    from lightglue_amd import mha_hd64_grouped
+
+    n0, n1 = 700, 513
+    (q0, k0, v0), (q1, k1, v1) = _group_inputs([(1, n0, n0), (1, n1, n1)], 31)
+    host = [(q0, k0, v0), (q1, k1, v1), (q0, k1, v1), (q1, k0, v0)]
+    dev_t = [tuple(_t(x, dev, torch.float16) for x in c) for c in host]
+    refs = [oracle_mod.attention_c(*c) for c in host]
+    for grouping in ([[0, 1], [2, 3]], [[0, 1, 2, 3]]):
+        outs = [None] * 4
+        for grp in grouping:
+            res = mha_hd64_grouped([dev_t[i] for i in grp])
+            for i, o in zip(grp, res):
+                outs[i] = o
+        torch.cuda.synchronize()
+        for i in range(4):
+            got = outs[i].float().cpu().numpy()
+            assert np.isfinite(got).all()
+            assert _maxdiff(got, refs[i]) <= TOL, (grouping, i)
+
+
+@pytest.mark.parametrize("in_dt,out_dt,tol", [(torch.float16, torch.float16, TOL),
+                                              (torch.float16, torch.float32, TOL_F32OUT),
+                                              (torch.float32, torch.float32, TOL)])
+def test_grouped_chunked_mixed_shapes(in_dt, out_dt, tol, dev, oracle_mod):
+    """Six calls (chunked 4 + 2) with mixed batch, tails, 1-row queries, and calls that split their
+    keys beside calls that do not (per-call split counts inside one launch + one combine)."""
+    from lightglue_amd import mha_hd64_grouped
+
+    shapes = [(1, 1, 1), (2, 100, 2048), (1, 1024, 64), (1, 33, 65), (3, 257, 1000), (1, 2048, 2048)]
+    host = _group_inputs(shapes, 55, np.float16 if in_dt == torch.float16 else np.float32)
+    dev_t = [tuple(_t(x, dev, in_dt) for x in c) for c in host]
+    outs = mha_hd64_grouped(dev_t, out_dtype=out_dt)
+    torch.cuda.synchronize()
+    for i, (c, o) in enumerate(zip(host, outs)):
+        rows = np.unique(np.r_[np.arange(0, c[0].shape[2], max(1, c[0].shape[2] // 40)), c[0].shape[2] - 1])
+        ref = oracle_mod.attention_c(np.ascontiguousarray(c[0][:, :, rows]), c[1], c[2])
+        got = o.float().cpu().numpy()
+        assert o.dtype == out_dt and np.isfinite(got).all(), i
+        assert _maxdiff(got[:, :, rows], ref) <= tol, i
+
+
+def test_grouped_matches_single_calls_bitwise_when_plans_agree(dev):
+    """A group of one is exactly the single-call launch (same plan, same kernel)."""
+    from lightglue_amd import mha_hd64_batched, mha_hd64_grouped, synth
+
+    qn, kn, vn = synth.qkv(9, 1024, 1024)
+    q, k, v = (_t(x, dev, torch.float16) for x in (qn, kn, vn))
+    a = mha_hd64_batched(q, k, v)
+    (b,) = mha_hd64_grouped([(q, k, v)])
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)

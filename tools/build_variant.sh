@@ -1,5 +1,6 @@
 #!/bin/bash
-# Build a library variant from a kernel source file (A/B experiments; never shipped):
+# Build a library variant from a kernel source file (A/B experiments; never shipped; PLUGIN_SRC=
+# an older shim source when the kernel source predates the current internal header):
 #   tools/build_variant.sh <kernel.hip> <name> [extra hipcc flags...]  -> lib/exp/libmha_hd64_<name>.so
 set -e
 SRC=$(readlink -f "$1"); NAME=$2; shift 2
@@ -8,6 +9,12 @@ mkdir -p lib/exp
 make -s lib/libmha_hd64.so
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans "$@" \
       -I../include -Icsrc -c "$SRC" -o lib/exp/k_$NAME.o
-hipcc --offload-arch=gfx950 -shared -fPIC lib/exp/k_$NAME.o lib/obj/mha_hd64_plugin.o -o lib/exp/libmha_hd64_$NAME.so
+PLUG=lib/obj/mha_hd64_plugin.o
+if [ -n "$PLUGIN_SRC" ]; then  # an older plugin shim for an older kernel source
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Icsrc -c "$(readlink -f "$PLUGIN_SRC")" -o lib/exp/p_$NAME.o
+  PLUG=lib/exp/p_$NAME.o
+fi
+hipcc --offload-arch=gfx950 -shared -fPIC lib/exp/k_$NAME.o $PLUG -o lib/exp/libmha_hd64_$NAME.so
+rm -f lib/exp/p_$NAME.o
 rm -f lib/exp/k_$NAME.o
 echo lib/exp/libmha_hd64_$NAME.so

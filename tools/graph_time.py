@@ -27,6 +27,8 @@ ROUNDS = 7
 def load(path):
     lib = ctypes.CDLL(os.path.abspath(path))
     for name, (args, res) in list(_lib.SIGNATURES.items()) + list(_lib.HOOKS.items()):
+        if not hasattr(lib, name):  # an older library build
+            continue
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res

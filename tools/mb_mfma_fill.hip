@@ -55,7 +55,10 @@ __global__ __launch_bounds__(512) void kern(const float* in, float* out, long lo
 #pragma unroll
     for (int i = 0; i < 16; ++i) s += acc0[i] + acc1[i] + x[i];
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
-    if (threadIdx.x % 64 == 0) cyc[blockIdx.x * 8 + threadIdx.x / 64] = t1 - t0;
+    if (threadIdx.x % 64 == 0) {
+        cyc[(blockIdx.x * 8 + threadIdx.x / 64) * 2] = t0;
+        cyc[(blockIdx.x * 8 + threadIdx.x / 64) * 2 + 1] = t1;
+    }
 }
 
 template <int KIND, int N, int MF>
@@ -63,14 +66,21 @@ void run(const char* name, float* in, float* out, long long* cyc, int threads) {
     hipLaunchKernelGGL((kern<KIND, N, MF>), dim3(256), dim3(threads), 0, 0, in, out, cyc);
     hipLaunchKernelGGL((kern<KIND, N, MF>), dim3(256), dim3(threads), 0, 0, in, out, cyc);
     hipDeviceSynchronize();
-    long long h[256 * 8];
+    long long h[256 * 8 * 2];
     hipMemcpy(h, cyc, sizeof(h), hipMemcpyDeviceToHost);
     double sum = 0;
     int nw = threads / 64;
-    for (int b = 0; b < 256; ++b)
-        for (int w = 0; w < nw; ++w) sum += h[b * 8 + w];
-    const double per = sum / (256.0 * nw) / (ITER * 8.0);
-    printf("%-8s N=%d mfma=%d waves/SIMD=%d : %.1f cyc per gap\n", name, N, MF, threads / 256, per);
+    for (int b = 0; b < 256; ++b) {
+        long long lo = h[(b * 8) * 2], hi = h[(b * 8) * 2 + 1];
+        for (int w = 0; w < nw; ++w) {
+            lo = h[(b * 8 + w) * 2] < lo ? h[(b * 8 + w) * 2] : lo;
+            hi = h[(b * 8 + w) * 2 + 1] > hi ? h[(b * 8 + w) * 2 + 1] : hi;
+        }
+        sum += hi - lo;
+    }
+    // block span per gap: for 2 waves/SIMD this covers both waves' MFMAs (2 per gap per SIMD)
+    const double per = sum / 256.0 / (ITER * 8.0);
+    printf("%-8s N=%d mfma=%d waves/SIMD=%d : %.1f cyc per gap (block span)\n", name, N, MF, threads / 256, per);
 }
 
 #define SWEEP(KIND, NAME, TH)                            \
@@ -87,13 +97,11 @@ int main() {
     long long* cyc;
     hipMalloc(&in, 4096 * 4);
     hipMalloc(&out, 256 * 512 * 4);
-    hipMalloc(&cyc, 256 * 8 * 8);
+    hipMalloc(&cyc, 256 * 8 * 8 * 2);
     hipMemset(in, 0, 4096 * 4);
     for (int th : {256, 512}) {
         SWEEP(0, "exp", th);
         SWEEP(1, "add", th);
-        SWEEP(2, "cvtpk", th);
-        SWEEP(3, "max3", th);
     }
     return 0;
 }
