@@ -32,6 +32,7 @@ struct Call {
 struct LaunchPlan {
     int q_waves;          // waves per workgroup that own distinct 32-row query slices
     int kv_waves;         // waves per workgroup that split the keys of every iteration
+    int rows_per_wave;    // 32, or 64 (two query blocks per wave)
     int splits;           // KV split across workgroups (1 = no combine pass)
     int tiles_per_split;  // KV super-tiles (64 * kv_waves keys) per split
     size_t ws_needed;     // workspace bytes the plan uses
@@ -45,6 +46,7 @@ constexpr int kGroupCalls = 4;
 struct GroupPlan {
     int q_waves;
     int kv_waves;
+    int rows_per_wave;  // 32 or 64 (two query blocks per wave share every K/V fragment read)
     int splits[kGroupCalls];
     int tiles_per_split[kGroupCalls];
     size_t ws_offset[kGroupCalls];
@@ -57,7 +59,8 @@ hipError_t launch_group(const Call* calls, int n, InType in, OutType out, void* 
                         int phase_mask = 3);
 size_t group_workspace_bytes(const Call* calls, int n);
 
-// Workgroup shapes compiled: (q_waves, kv_waves) in {(4,1), (2,2), (1,2), (4,2)}.
+// Workgroup shapes compiled: (q_waves, kv_waves) in {(4,1), (2,2), (1,2), (4,2)} with 32-row waves,
+// and (2,2) with 64-row waves (forced as q_waves = 12).
 LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves = 0, int force_kv_waves = 0,
                      int force_splits = 0);
 size_t split_workspace_bytes(const Call& c, int splits);

@@ -128,15 +128,19 @@ __device__ __forceinline__ float xhalf_max(float x) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
+// Row max of the 32 scores of a lane as a v_max3_f32 tree (16 instructions: 11 + 4 + 1).
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 __device__ __forceinline__ float tree_max(const f32x16& a, const f32x16& b) {
-    float t[16];
+    float t[11];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) t[i] = fmaxf(a[i], b[i]);
+    for (int i = 0; i < 5; ++i) t[i] = max3f(a[3 * i], a[3 * i + 1], a[3 * i + 2]);
+    t[5] = max3f(a[15], b[0], b[1]);
 #pragma unroll
-    for (int w = 8; w >= 1; w >>= 1)
-#pragma unroll
-        for (int i = 0; i < w; ++i) t[i] = fmaxf(t[i], t[i + w]);
-    return t[0];
+    for (int i = 0; i < 4; ++i) t[6 + i] = max3f(b[2 + 3 * i], b[3 + 3 * i], b[4 + 3 * i]);
+    t[10] = fmaxf(b[14], b[15]);
+    const float u0 = max3f(t[0], t[1], t[2]), u1 = max3f(t[3], t[4], t[5]);
+    const float u2 = max3f(t[6], t[7], t[8]), u3 = fmaxf(t[9], t[10]);
+    return fmaxf(max3f(u0, u1, u2), u3);
 }
 // LDS accesses through an explicit address-space-3 base and 32-bit byte offsets, so the
 // compiler folds the compile-time part of every address into the DS instruction's offset field.
@@ -186,6 +190,8 @@ __device__ __forceinline__ f32x16 splat16(float x) {
 #define ABL_NO_QK 32
 #define ABL_NO_GLOAD 64   // no K/V/Q global loads (LDS and Q hold garbage)
 #define ABL_NO_STORE 128  // no output / partial stores
+#define ABL_K_CONST 256   // K fragments from registers (no K LDS reads)
+#define ABL_V_CONST 512   // V fragments from registers (no V LDS reads)
 __device__ __forceinline__ void keep_live(const f16x8& x) { asm volatile("" ::"v"(x)); }
 
 // In-kernel timestamps (diagnostic build -DMHA_STAMPS only): s_memtime after draining memory.
@@ -224,6 +230,11 @@ __device__ __forceinline__ void keep_live(const f16x8& x) { asm volatile("" ::"v
 #define TCLK(var) \
     do {          \
     } while (0)
+#endif
+
+#ifndef MHA_PINGPONG
+#define MHA_PINGPONG 0  // measured neutral on the steady loop (vector-issue bound), and it makes the
+                        // fp32-input 8-wave kernel spill: off by default, kept as a switch
 #endif
 
 constexpr float kMaskBias = -65504.f;  // fp16 lowest: a masked key's score, exp2 -> 0
@@ -268,13 +279,23 @@ __device__ __forceinline__ void bload8(Raw8<float>& r, __amdgpu_buffer_rsrc_t rs
 // ----------------------------------------------------------------------------------------
 // MULTI = false: a launch of one call (plugin enqueue, L0 launchers) reads only c[0], so the
 // prologue's kernarg loads issue in one scalar round; MULTI = true: grouped launches.
-template <typename TIn, typename TOut, int QW, int KW, bool MULTI>
+// RB = 32-row query blocks per wave: RB = 2 shares every K/V fragment read between two
+// query blocks (half the LDS read traffic per FLOP), at twice the registers per wave.
+template <typename TIn, typename TOut, int QW, int KW, int RB, bool MULTI>
 __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a) {
     constexpr int NT = 64 * QW * KW;                // threads
-    constexpr int BLOCK_M = 32 * QW;                // query rows per workgroup
+    constexpr int BLOCK_M = 32 * QW * RB;           // query rows per workgroup
     constexpr int SUPER = kTileKV * KW;             // keys per iteration
     constexpr int STAGE_BYTES = KW * 2 * kTileBytes;
-    constexpr int NSTAGE = 3;
+    // LDS ring of super-tiles: step t reads K(t+1) and V(t) and refills super-tile t + NSTAGE-1.
+    // Ping-pong (8-wave workgroups, two waves per SIMD; cdna_hip_programming.md T16): every step is a
+    // load segment (all LDS reads / writes) and a compute segment (all MFMAs + softmax, from
+    // registers), separated by a barrier; waves 4-7 run one segment behind waves 0-3, so each
+    // SIMD pairs one wave's matrix work with its partner's memory work. 4-wave shapes keep one
+    // barrier per step with the LDS work spread over the step.
+    constexpr bool PINGPONG = (NT == 512) && (MHA_PINGPONG != 0);
+    // Offset halves read one segment apart, so the ping-pong ring needs a fourth stage.
+    constexpr int NSTAGE = PINGPONG ? 4 : 3;
     constexpr int NLOAD = (2 * KW * 512) / NT;      // 16-B chunks staged per thread per iteration
     constexpr unsigned SZ = sizeof(TIn);
     static_assert(NLOAD * NT == 2 * KW * 512, "staging must divide evenly");
@@ -323,7 +344,7 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     const __amdgpu_buffer_rsrc_t q_rs = make_rsrc(Qb, (unsigned)nq * kHeadDim * SZ);
     const __amdgpu_buffer_rsrc_t k_rs = make_rsrc(Kb, (unsigned)nkv * kHeadDim * SZ);
     const __amdgpu_buffer_rsrc_t v_rs = make_rsrc(Vb, (unsigned)nkv * kHeadDim * SZ);
-    const int q_row = qtile * BLOCK_M + qw * 32 + r;
+    const int q_row0 = qtile * BLOCK_M + qw * 32 * RB + r;  // + 32 * rb
 
     const int super_total = (nkv + SUPER - 1) / SUPER;
     const int st_begin = split * ca.tiles_per_split;
@@ -335,8 +356,8 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     // choice stays scalar (no waterfall loop around the buffer load).
     constexpr int PER = 512 / NT;  // loads per thread per 8 KiB tile-tensor
     static_assert(PER * NT == 512, "workgroup size must divide a tile");
-    // Two staging register sets: the loads of super-tile t+3 are issued at step t (two steps
-    // of latency cover for first-touch MALL/HBM reads) while set t+2 is written to LDS.
+    // Two staging register sets: the loads of super-tile t+NSTAGE are issued at step t while the
+    // set holding super-tile t+NSTAGE-1 is written to LDS.
     Raw8<TIn> stgA[NLOAD], stgB[NLOAD];
     auto issue = [&](int it, Raw8<TIn>(&stg)[NLOAD]) {
         if (MHA_ABL & ABL_NO_GLOAD) {
@@ -365,19 +386,21 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     };
 
     // Q fragments (B operand of Sᵀ = K·Qᵀ): lane holds Q[q_row][16s + 8hh .. +7] * 0.125*log2(e), fp16.
-    f16x8 qf[4];
+    f16x8 qf[RB][4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        Raw8<TIn> t;
-        if (MHA_ABL & ABL_NO_GLOAD) t = Raw8<TIn>{};
-        else bload8(t, q_rs, (unsigned)(q_row * kHeadDim + 16 * s + 8 * hh) * SZ, 0);
-        const f16x8 h = to_f16(t);
+    for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) qf[s][e] = (f16)((float)h[e] * kScaleLog2);
-    }
+        for (int s = 0; s < 4; ++s) {
+            Raw8<TIn> t;
+            if (MHA_ABL & ABL_NO_GLOAD) t = Raw8<TIn>{};
+            else bload8(t, q_rs, (unsigned)((q_row0 + 32 * rb) * kHeadDim + 16 * s + 8 * hh) * SZ, 0);
+            const f16x8 h = to_f16(t);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) qf[rb][s][e] = (f16)((float)h[e] * kScaleLog2);
+        }
 
-    // Prologue: stage 0 is published first so QKᵀ(0) starts while stage 1 is still in flight
-    // (stage 1 is written and published right after it); super-tile 2 goes in flight in set A.
+    // Prologue: stage 0 is published first so QKᵀ(0) starts while the next stage(s) are in flight
+    // (published right after it).
     if (n_iter > 0) issue(0, stgA);
     if (n_iter > 1) issue(1, stgB);
     if (n_iter > 0) write(0, stgA);
@@ -397,7 +420,7 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     const unsigned v_addr0 = v_lane + 64 * vb + (kw * 2 + 1) * kTileBytes;        // dims 0..31
     const unsigned v_addr1 = v_lane + 64 * (1 - vb) + (kw * 2 + 1) * kTileBytes;  // dims 32..63
 
-    float m_run = 0.f;        // reference max of this lane's query, log2 units (s·c)
+    float m_run[RB];          // reference max of this lane's query, log2 units (s·c)
     // Row sums on the matrix pipe: l_acc = ones_sel · P over every k-step (16x16x32 MFMA), so the
     // 31 adds per tile leave the vector pipe. P (the 32x32x16 B operand) read as a 16x16x32 B
     // operand puts query n (lanes 0-15, 32-47) and n+16 (lanes 16-31, 48-63) in column n; the
@@ -405,7 +428,7 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     // the sum of query l&31 over the step's 16 keys (both half-waves) — the lane's own query.
     const f16 sel = (((lane & 15) >> 2) & 1) == ((lane >> 4) & 1) ? (f16)1.f : (f16)0.f;
     const f16x8 a_sum = f16x8{sel, sel, sel, sel, sel, sel, sel, sel};
-    f32x4 l_acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 l_acc[RB];
     // Bias k-step of the QKᵀ chains: A (key side) = [1, 1, mask] per key row, B (query side) =
     // [-m_hi, -m_lo, 1] per query, in k-slots 0..2 of the lower half-wave (zeros elsewhere).
     // One extra MFMA per chain adds -m (fp16 hi + lo, error ~|m|·2^-22) and the tail mask, so
@@ -413,16 +436,29 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     // subtraction and no masking VALU.
     const f16 one_h = hh == 0 ? (f16)1.f : (f16)0.f;
     const f16x8 a_bias = f16x8{one_h, one_h, 0, 0, 0, 0, 0, 0};
-    f16x8 b_bias = f16x8{0, 0, one_h, 0, 0, 0, 0, 0};  // m_run = 0
-    auto set_bias = [&]() {
-        const f16 hi = (f16)(-m_run);
-        const f16 lo = (f16)(-m_run - (float)hi);
-        b_bias = hh == 0 ? f16x8{hi, lo, (f16)1.f, 0, 0, 0, 0, 0} : f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    f16x8 b_bias[RB];
+    auto set_bias = [&](int rb) {
+        const f16 hi = (f16)(-m_run[rb]);
+        const f16 lo = (f16)(-m_run[rb] - (float)hi);
+        b_bias[rb] = hh == 0 ? f16x8{hi, lo, (f16)1.f, 0, 0, 0, 0, 0} : f16x8{0, 0, 0, 0, 0, 0, 0, 0};
     };
-    f32x16 o0 = {}, o1 = {};  // Oᵀ tiles: dims 0..31 and 32..63, query on the lane
+    f32x16 o0[RB], o1[RB];  // Oᵀ tiles: dims 0..31 and 32..63, query on the lane
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+        m_run[rb] = 0.f;
+        l_acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        b_bias[rb] = f16x8{0, 0, one_h, 0, 0, 0, 0, 0};  // m_run = 0
+        o0[rb] = f32x16{};
+        o1[rb] = f32x16{};
+    }
 
     // K fragments of the tile in stage kstage (A operand of Sᵀ = K·Qᵀ, 8 x ds_read_b128).
     auto read_k = [&](unsigned kstage, f16x8(&kf)[8]) {
+        if (MHA_ABL & ABL_K_CONST) {
+#pragma unroll
+            for (int s = 0; s < 8; ++s) kf[s] = qf[0][s & 3];
+            return;
+        }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const unsigned ka = k_addr[s] + kstage;
@@ -433,7 +469,8 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     // QKᵀ chain step i (0..9) of the tile: i = 0,1 are the bias k-steps of the two 32-key halves,
     // then K·Qᵀ over the 4 dim k-steps alternating halves. Scores s·c - m (log2 units), masked
     // keys at ~-65504. Split per MFMA so the caller can interleave vector work between them.
-    auto qk_step = [&](int i, const f16x8(&kf)[8], const f16x8& ab0, const f16x8& ab1, f32x16& s0, f32x16& s1) {
+    auto qk_step = [&](int i, const f16x8(&kf)[8], const f16x8& ab0, const f16x8& ab1, f32x16& s0, f32x16& s1,
+                       int rb) {
         const f32x16 zero = {};
         if (MHA_ABL & ABL_NO_QK) {
             if (i == 0) s0 = zero;
@@ -441,16 +478,19 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
             if (i >= 2) keep_live(kf[i - 2]);
             return;
         }
-        if (i == 0) s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab0, b_bias, zero, 0, 0, 0);
-        else if (i == 1) s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab1, b_bias, zero, 0, 0, 0);
-        else if ((i & 1) == 0) s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[i - 2], qf[(i - 2) >> 1], s0, 0, 0, 0);
-        else s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[i - 2], qf[(i - 2) >> 1], s1, 0, 0, 0);
+        if (i == 0) s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab0, b_bias[rb], zero, 0, 0, 0);
+        else if (i == 1) s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab1, b_bias[rb], zero, 0, 0, 0);
+        else if ((i & 1) == 0)
+            s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[i - 2], qf[rb][(i - 2) >> 1], s0, 0, 0, 0);
+        else s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[i - 2], qf[rb][(i - 2) >> 1], s1, 0, 0, 0);
     };
-    auto qk = [&](unsigned kstage, const f16x8& ab0, const f16x8& ab1, f32x16& s0, f32x16& s1) {
+    auto qk = [&](unsigned kstage, const f16x8& ab0, const f16x8& ab1, f32x16(&s0)[RB], f32x16(&s1)[RB]) {
         f16x8 kf[8];
         read_k(kstage, kf);
 #pragma unroll
-        for (int i = 0; i < 10; ++i) qk_step(i, kf, ab0, ab1, s0, s1);
+        for (int i = 0; i < 10; ++i)
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) qk_step(i, kf, ab0, ab1, s0[rb], s1[rb], rb);
     };
     // Tail mask (reference: last KV tile only, …fp16out.cu:475-494): the bias A operand of the
     // tile carries kMaskBias in k-slot 2 for key rows >= nkv. Only the last super-tile of the
@@ -462,52 +502,45 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     };
     const bool tail = (st_begin + n_iter) * SUPER > nkv;  // last super-tile of this split is partial
 
-    // Ring stage of tile `it` (scalar, advanced once per step: no modulo per access).
+    // Ring stage of tile `it` (scalar, advanced once per step).
     int st_cur = 0;
-    auto next_stage = [](int st) { return st == NSTAGE - 1 ? 0 : st + 1; };
-    // Step `it` writes super-tile it+2 from set `wr` and issues super-tile it+3 into set `is`.
+    // Step `it` writes super-tile it+3 from set `wr` and issues super-tile it+4 into set `is`.
 #ifdef MHA_STEPSTAMPS
     unsigned long long ck[4] = {}, ck_prev[4] = {}, ck_sum[4] = {};
     bool ck_first = true;
 #endif
-    auto step = [&](int it, f32x16& c0, f32x16& c1, float mxc, f32x16& n0, f32x16& n1, float& mxn,
+    auto step = [&](int it, f32x16(&c0)[RB], f32x16(&c1)[RB], const float(&mxc)[RB], f32x16(&n0)[RB],
+                    f32x16(&n1)[RB], float(&mxn)[RB],
                     auto has_next_c, bool mask_next, Raw8<TIn>(&wr)[NLOAD], Raw8<TIn>(&is)[NLOAD],
-                    bool may_issue) {
+                    bool may_issue, bool may_write) {
         constexpr bool HAS_NEXT = decltype(has_next_c)::value;
-        const int st_nxt = next_stage(st_cur);
-        const int st_fill = next_stage(st_nxt);
-        // In the steady loop the refill is unconditional (may_issue = true at compile time): a load
-        // past this split's last super-tile is never written to LDS, and past nkv the buffer
-        // descriptor returns zeros. A conditional load would make the compiler's vmcnt analysis
-        // drain every load at the next LDS write (a one-step prefetch instead of two).
-        if (!(MHA_ABL & ABL_NO_REFILL) && may_issue) issue(it + 3, is);
+        const int st_nxt = st_cur == NSTAGE - 1 ? 0 : st_cur + 1;
+        const int st_fill = st_cur == 0 ? NSTAGE - 1 : st_cur - 1;  // (st_cur + NSTAGE-1) mod NSTAGE
+        // In the steady loop the refill is unconditional (may_issue = true at compile time): a
+        // super-tile past this split's last one lands in a stage nobody reads, and past nkv the
+        // buffer descriptor returns zeros. A conditional load would make the compiler's vmcnt
+        // analysis drain every load at the next LDS write.
+        if (!(MHA_ABL & ABL_NO_REFILL) && may_issue) issue(it + NSTAGE, is);
         TCLK(ck[0]);
-
-        // online-softmax decision for tile `it` (first tile: set the max exactly; later tiles:
-        // move it only when some query's tile max exceeds it by > kRescaleThr)
-        const bool first = (it == 0);
-        if (first || __builtin_amdgcn_ballot_w64(mxc > kRescaleThr) != 0) {  // wave-uniform, rare
-            const float d = first ? ((mxc < kEmptyMax) ? 0.f : mxc)  // a fully masked tile keeps m = 0
-                                  : fmaxf(mxc, 0.f);
-            const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-d);
-            o0 *= alpha;
-            o1 *= alpha;
-            l_acc *= alpha;
-            m_run += d;
-            c0 -= d;
-            c1 -= d;
-            set_bias();
-        }
 
         // Fragment reads first: K of tile it+1 (phase A) and Vᵀ of tile it (phase B); both stages
         // are complete since the last barrier, and the reads land while the bias MFMAs run.
         f16x8 kf[8];
-        if constexpr (HAS_NEXT) read_k((unsigned)st_nxt * STAGE_BYTES, kf);
         // (8-wave workgroups with fp32 staging registers read Vᵀ in phase B instead: the early
         // reads' 32 VGPRs would spill there.)
         constexpr bool kEarlyV = !(NT == 512 && SZ == 4);
         f16x8 vfa[2][2], vfb[2][2];
         auto read_v = [&]() {
+            if (MHA_ABL & ABL_V_CONST) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int ss = 0; ss < 2; ++ss) {
+                        vfa[j][ss] = qf[0][j + 2 * ss];
+                        vfb[j][ss] = qf[0][(j + 2 * ss + 1) & 3];
+                    }
+                return;
+            }
             const unsigned va0 = v_addr0 + (unsigned)st_cur * STAGE_BYTES;
             const unsigned va1 = v_addr1 + (unsigned)st_cur * STAGE_BYTES;
 #pragma unroll
@@ -519,71 +552,114 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
                     vfb[j][ss] = cat8(tr_read(lds, va1 + rowc), tr_read(lds, va1 + rowc + 8 * 128));
                 }
         };
-        if constexpr (kEarlyV && !HAS_NEXT) read_v();
+        if constexpr (PINGPONG) {
+            // Load segment (ping-pong): every LDS access of the step — K(it+1) and Vᵀ(it) fragments
+            // into registers, the refill of super-tile it+3 — while the partner wave on this SIMD
+            // runs its compute segment; the barrier's lgkmcnt(0) lands them all.
+            if constexpr (HAS_NEXT) read_k((unsigned)st_nxt * STAGE_BYTES, kf);
+            read_v();
+            if (!(MHA_ABL & ABL_NO_REFILL) && may_write) write(st_fill, wr);
+            if (!(MHA_ABL & ABL_NO_BARRIER)) __syncthreads();
+        }
+
+        // online-softmax decision for tile `it` (first tile: set the max exactly; later tiles:
+        // move it only when some query's tile max exceeds it by > kRescaleThr)
+        const bool first = (it == 0);
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            if (first || __builtin_amdgcn_ballot_w64(mxc[rb] > kRescaleThr) != 0) {  // wave-uniform, rare
+                const float d = first ? ((mxc[rb] < kEmptyMax) ? 0.f : mxc[rb])  // fully masked tile: m = 0
+                                      : fmaxf(mxc[rb], 0.f);
+                const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-d);
+                o0[rb] *= alpha;
+                o1[rb] *= alpha;
+                l_acc[rb] *= alpha;
+                m_run[rb] += d;
+                c0[rb] -= d;
+                c1[rb] -= d;
+                set_bias(rb);
+            }
+        }
+
+        if constexpr (!PINGPONG) {
+            if constexpr (HAS_NEXT) read_k((unsigned)st_nxt * STAGE_BYTES, kf);
+            if constexpr (kEarlyV && !HAS_NEXT) read_v();
+        }
 
         // phase A: QKᵀ(it+1) on the matrix pipe ‖ exp(it) on the vector pipe, pinned as one MFMA
         // followed by three v_exp_f32 per gap (8 + 3·8 issue cycles fill the MFMA's 32).
-        auto exp_at = [&](int e) {
+        auto exp_at = [&](int e) {  // e in [0, 32*RB): query block e/32, score e%32
             if (MHA_ABL & (ABL_NO_EXP | ABL_NO_SOFTMAX)) return;
-            if (e < 16) c0[e] = __builtin_amdgcn_exp2f(c0[e]);
-            else c1[e - 16] = __builtin_amdgcn_exp2f(c1[e - 16]);
+            const int rb = e >> 5, i = e & 31;
+            if (i < 16) c0[rb][i] = __builtin_amdgcn_exp2f(c0[rb][i]);
+            else c1[rb][i - 16] = __builtin_amdgcn_exp2f(c1[rb][i - 16]);
         };
         if constexpr (HAS_NEXT) {
             const f16x8 ab0 = mask_next ? a_bias_tile(it + 1, 0) : a_bias;
             const f16x8 ab1 = mask_next ? a_bias_tile(it + 1, 1) : a_bias;
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int i = 0; i < 10; ++i) {
-                qk_step(i, kf, ab0, ab1, n0, n1);
-                // Vᵀ reads queue behind the K reads (phase A carries all fragment reads).
-                if (kEarlyV && i == 2) read_v();
-                exp_at(3 * i);
-                exp_at(3 * i + 1);
-                exp_at(3 * i + 2);
-                __builtin_amdgcn_sched_barrier(0);
-            }
+            for (int i = 0; i < 10; ++i)
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) {
+                    qk_step(i, kf, ab0, ab1, n0[rb], n1[rb], rb);
+                    // Vᵀ reads queue behind the K reads (phase A carries all fragment reads).
+                    if (!PINGPONG && kEarlyV && i == 2 && rb == 0) read_v();
+                    const int g = i * RB + rb;
+                    exp_at(3 * g);
+                    exp_at(3 * g + 1);
+                    exp_at(3 * g + 2);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             TCLK(ck[1]);
-            exp_at(30);
-            exp_at(31);
+#pragma unroll
+            for (int e = 30 * RB; e < 32 * RB; ++e) exp_at(e);
         } else {
 #pragma unroll
-            for (int e = 0; e < 32; ++e) exp_at(e);
+            for (int e = 0; e < 32 * RB; ++e) exp_at(e);
         }
-        f16x8 p[2][2];  // P (f16) as the B operand: registers 8ss..8ss+7 of a 32x32 tile = k-step ss
+        f16x8 p[RB][2][2];  // P (f16) as the B operand: registers 8ss..8ss+7 of a 32x32 tile = k-step ss
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            p[0][0][e] = (f16)c0[e];
-            p[0][1][e] = (f16)c0[8 + e];
-            p[1][0][e] = (f16)c1[e];
-            p[1][1][e] = (f16)c1[8 + e];
-        }
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                p[rb][0][0][e] = (f16)c0[rb][e];
+                p[rb][0][1][e] = (f16)c0[rb][8 + e];
+                p[rb][1][0][e] = (f16)c1[rb][e];
+                p[rb][1][1][e] = (f16)c1[rb][8 + e];
+            }
 
-        // phase B: Oᵀ += Vᵀ·Pᵀ (it) and the row sums on the matrix pipe ‖ row max (it+1) and the
-        // LDS refill of stage it+2 (free since the last barrier): phase A is LDS-read bound, so
-        // the refill's LDS writes go here, where the LDS is otherwise idle.
-        if constexpr (!kEarlyV) read_v();
-        if (HAS_NEXT && !(MHA_ABL & ABL_NO_REFILL) && it + 2 < n_iter) write(st_fill, wr);
+        // phase B: Oᵀ += Vᵀ·Pᵀ (it) and the row sums on the matrix pipe ‖ row max (it+1) (and, in
+        // the one-barrier form, the LDS refill of super-tile it+3: its stage held tile it-1).
+        if constexpr (!PINGPONG) {
+            if constexpr (!kEarlyV) read_v();
+            if (!(MHA_ABL & ABL_NO_REFILL) && may_write) write(st_fill, wr);
+        }
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                if (MHA_ABL & ABL_NO_PV) {
-                    keep_live(vfa[j][ss]);
-                    keep_live(vfb[j][ss]);
-                    keep_live(p[j][ss]);
-                } else {
-                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa[j][ss], p[j][ss], o0, 0, 0, 0);
-                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb[j][ss], p[j][ss], o1, 0, 0, 0);
+            for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) {
+                    if (MHA_ABL & ABL_NO_PV) {
+                        keep_live(vfa[j][ss]);
+                        keep_live(vfb[j][ss]);
+                        keep_live(p[rb][j][ss]);
+                    } else {
+                        o0[rb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa[j][ss], p[rb][j][ss], o0[rb], 0, 0, 0);
+                        o1[rb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb[j][ss], p[rb][j][ss], o1[rb], 0, 0, 0);
+                    }
+                    if (!(MHA_ABL & ABL_NO_SOFTMAX))
+                        l_acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, p[rb][j][ss], l_acc[rb], 0, 0, 0);
                 }
-                if (!(MHA_ABL & ABL_NO_SOFTMAX))
-                    l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, p[j][ss], l_acc, 0, 0, 0);
-            }
         if constexpr (HAS_NEXT) {
-            if (MHA_ABL & ABL_NO_SOFTMAX) mxn = 0.f;
-            else mxn = xhalf_max(tree_max(n0, n1));
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) {
+                if (MHA_ABL & ABL_NO_SOFTMAX) mxn[rb] = 0.f;
+                else mxn[rb] = xhalf_max(tree_max(n0[rb], n1[rb]));
+            }
         }
 
-        if (!HAS_NEXT && !(MHA_ABL & ABL_NO_REFILL) && it + 2 < n_iter) write(st_fill, wr);
         TCLK(ck[2]);
 #ifdef MHA_STEPSTAMPS
         if (HAS_NEXT) {  // previous full step's phases (its clocks have returned by now)
@@ -604,8 +680,10 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     };
 
     // Scores ping-pong between two named register sets (no runtime-indexed arrays, no copies).
-    f32x16 sA0, sA1, sB0, sB1;
-    float mxA = 0.f, mxB = 0.f;
+    f32x16 sA0[RB], sA1[RB], sB0[RB], sB1[RB];
+    float mxA[RB], mxB[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) mxA[rb] = mxB[rb] = 0.f;
     using T_ = std::true_type;
     using F_ = std::false_type;
     if (n_iter > 0) {
@@ -613,35 +691,50 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
             qk(0u, a_bias_tile(0, 0), a_bias_tile(0, 1), sA0, sA1);
         else
             qk(0u, a_bias, a_bias, sA0, sA1);
-        mxA = xhalf_max(tree_max(sA0, sA1));
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) mxA[rb] = xhalf_max(tree_max(sA0[rb], sA1[rb]));
     }
-    if (n_iter > 1) {
-        write(1, stgB);
-        __syncthreads();
+    if (n_iter > 1) write(1, stgB);
+    if constexpr (NSTAGE == 4) {
+        if (n_iter > 3) issue(3, stgB);
+        if (n_iter > 2) write(2, stgA);
     }
+    if (n_iter > 1) __syncthreads();
+    // The set the first step writes from (super-tile NSTAGE-1) and the one it issues into.
+    Raw8<TIn>(&stg0)[NLOAD] = NSTAGE == 4 ? stgB : stgA;
+    Raw8<TIn>(&stg1)[NLOAD] = NSTAGE == 4 ? stgA : stgB;
 #ifndef MHA_PRIO
-#define MHA_PRIO 1
+#define MHA_PRIO 0
 #endif
-    // Two waves per SIMD: the second-dispatched half loses every age-ordered issue arbitration
-    // and arrives last at each barrier; static priority for that half evens the two out.
+    // (static priority for the second-dispatched half of an 8-wave workgroup: diagnostic switch)
     if (MHA_PRIO && NT == 512 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+    // Ping-pong offset: the second half starts one phase late (one extra barrier before the loop,
+    // matched by one extra barrier of the first half after it).
+    const bool late_half = PINGPONG && wave >= 4;
+    if (late_half) __syncthreads();
     int it = 0;
     // Steady state: tiles it+1 and it+2 exist and neither is the (possibly partial) last one.
+    // Refill issue / write are unconditional here (see step).
     for (; it + 3 < n_iter; it += 2) {
-        step(it, sA0, sA1, mxA, sB0, sB1, mxB, T_{}, false, stgA, stgB, true);
-        step(it + 1, sB0, sB1, mxB, sA0, sA1, mxA, T_{}, false, stgB, stgA, true);
+        step(it, sA0, sA1, mxA, sB0, sB1, mxB, T_{}, false, stg0, stg1, true, true);
+        step(it + 1, sB0, sB1, mxB, sA0, sA1, mxA, T_{}, false, stg1, stg0, true, true);
     }
     // Tail (at most 3 iterations): same step with the mask flag live; scores and the pending
-    // staging set move back to A after each step.
+    // staging set move back after each step.
     for (; it + 1 < n_iter; ++it) {
-        step(it, sA0, sA1, mxA, sB0, sB1, mxB, T_{}, tail && (it + 2 == n_iter), stgA, stgB, it + 3 < n_iter);
-        sA0 = sB0;
-        sA1 = sB1;
-        mxA = mxB;
+        step(it, sA0, sA1, mxA, sB0, sB1, mxB, T_{}, tail && (it + 2 == n_iter), stg0, stg1, it + NSTAGE < n_iter,
+             it + NSTAGE - 1 < n_iter);
 #pragma unroll
-        for (int i = 0; i < NLOAD; ++i) stgA[i] = stgB[i];
+        for (int rb = 0; rb < RB; ++rb) {
+            sA0[rb] = sB0[rb];
+            sA1[rb] = sB1[rb];
+            mxA[rb] = mxB[rb];
+        }
+#pragma unroll
+        for (int i = 0; i < NLOAD; ++i) stg0[i] = stg1[i];
     }
-    if (it < n_iter) step(it, sA0, sA1, mxA, sB0, sB1, mxB, F_{}, false, stgA, stgB, false);
+    if (it < n_iter) step(it, sA0, sA1, mxA, sB0, sB1, mxB, F_{}, false, stg0, stg1, false, false);
+    if (PINGPONG && !late_half) __syncthreads();
     STAMP(2);
 
     // ---- epilogue ----
@@ -650,21 +743,23 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     // chunks (a wave stores complete rows: coalesced, few store instructions).
     // A wave that saw no key (all of its tiles past nkv) gets m = -inf (weight 0). The test uses
     // the cross-half total: the halves hold disjoint keys but the SAME query's m and O dims.
-    const float L_w = l_acc[0];  // the row-sum MFMA already spans both half-waves
-    const float m_w = (L_w > 0.f) ? m_run : -INFINITY;
     constexpr int OROW = 68;  // fp32 row pitch in LDS: 64 dims + 4 pad (rows r, r+1 on different banks)
     float* ol = reinterpret_cast<float*>(smem);     // [KW][BLOCK_M][OROW]
     float* mlb = ol + KW * BLOCK_M * OROW;          // [KW][BLOCK_M][2]
     static_assert((KW * BLOCK_M * OROW + KW * BLOCK_M * 2) * 4 <= NSTAGE * STAGE_BYTES, "epilogue LDS");
-    {
-        const int row = qw * 32 + r;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+        const float L_w = l_acc[rb][0];  // the row-sum MFMA already spans both half-waves
+        const float m_w = (L_w > 0.f) ? m_run[rb] : -INFINITY;
+        const int row = qw * 32 * RB + 32 * rb + r;
         float* dst = ol + (kw * BLOCK_M + row) * OROW;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
             const int d = 8 * g4 + 4 * hh;
-            *reinterpret_cast<f32x4*>(dst + d) = f32x4{o0[4 * g4], o0[4 * g4 + 1], o0[4 * g4 + 2], o0[4 * g4 + 3]};
+            *reinterpret_cast<f32x4*>(dst + d) =
+                f32x4{o0[rb][4 * g4], o0[rb][4 * g4 + 1], o0[rb][4 * g4 + 2], o0[rb][4 * g4 + 3]};
             *reinterpret_cast<f32x4*>(dst + 32 + d) =
-                f32x4{o1[4 * g4], o1[4 * g4 + 1], o1[4 * g4 + 2], o1[4 * g4 + 3]};
+                f32x4{o1[rb][4 * g4], o1[rb][4 * g4 + 1], o1[rb][4 * g4 + 2], o1[rb][4 * g4 + 3]};
         }
         if (hh == 0) *reinterpret_cast<float2*>(mlb + (kw * BLOCK_M + row) * 2) = make_float2(m_w, L_w);
     }
@@ -838,27 +933,30 @@ __global__ __launch_bounds__(256) void mha_hd64_combine_kernel(CombineArgs c) {
     store4<TOut>(out, acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
 }
 
-template <typename TIn, typename TOut, int QW, int KW, bool MULTI>
+template <typename TIn, typename TOut, int QW, int KW, int RB, bool MULTI>
 hipError_t launch_fwd(const FwdArgs& a, int grid, hipStream_t stream) {
-    hipLaunchKernelGGL((mha_hd64_fwd_kernel<TIn, TOut, QW, KW, MULTI>), dim3(grid), dim3(64 * QW * KW), 0, stream, a);
+    hipLaunchKernelGGL((mha_hd64_fwd_kernel<TIn, TOut, QW, KW, RB, MULTI>), dim3(grid), dim3(64 * QW * KW), 0, stream,
+                       a);
     return hipGetLastError();
 }
 
 // Grouped launches (several calls) exist for the two shapes the planner picks on its own.
 template <typename TIn, typename TOut>
-hipError_t launch_fwd_shape(const FwdArgs& a, int grid, int qw, int kw, hipStream_t stream) {
+hipError_t launch_fwd_shape(const FwdArgs& a, int grid, int qw, int kw, int rb, hipStream_t stream) {
     if (a.n_calls > 1) {
-        switch (qw * 8 + kw) {
-            case 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, true>(a, grid, stream);
-            case 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2, true>(a, grid, stream);
+        switch (rb * 64 + qw * 8 + kw) {
+            case 64 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 1, true>(a, grid, stream);
+            case 64 + 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2, 1, true>(a, grid, stream);
+            case 128 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 2, true>(a, grid, stream);
             default: return hipErrorInvalidValue;
         }
     }
-    switch (qw * 8 + kw) {
-        case 4 * 8 + 1: return launch_fwd<TIn, TOut, 4, 1, false>(a, grid, stream);
-        case 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, false>(a, grid, stream);
-        case 1 * 8 + 2: return launch_fwd<TIn, TOut, 1, 2, false>(a, grid, stream);
-        case 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2, false>(a, grid, stream);
+    switch (rb * 64 + qw * 8 + kw) {
+        case 64 + 4 * 8 + 1: return launch_fwd<TIn, TOut, 4, 1, 1, false>(a, grid, stream);
+        case 64 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 1, false>(a, grid, stream);
+        case 64 + 1 * 8 + 2: return launch_fwd<TIn, TOut, 1, 2, 1, false>(a, grid, stream);
+        case 64 + 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2, 1, false>(a, grid, stream);
+        case 128 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 2, false>(a, grid, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -872,8 +970,9 @@ hipError_t launch_combine(const CombineArgs& c, hipStream_t stream) {
     return hipGetLastError();
 }
 
-bool valid_shape(int qw, int kw) {
-    return (qw == 4 && kw == 1) || (qw == 2 && kw == 2) || (qw == 1 && kw == 2) || (qw == 4 && kw == 2);
+bool valid_shape(int qw, int kw, int rb) {
+    if (rb == 2) return qw == 2 && kw == 2;
+    return rb == 1 && ((qw == 4 && kw == 1) || (qw == 2 && kw == 2) || (qw == 1 && kw == 2) || (qw == 4 && kw == 2));
 }
 
 unsigned long long* g_stamps = nullptr;  // diagnostic builds (MHA_STAMPS) only
@@ -894,8 +993,11 @@ size_t split_workspace_bytes(const Call& c, int splits) {
 GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_waves, int force_kv_waves,
                      int force_splits) {
     GroupPlan p{};
-    int qw = force_q_waves, kw = force_kv_waves;
-    if (!valid_shape(qw, kw)) {
+    // Forced shapes (test/bench hook): q_waves >= 10 selects 64-row waves (RB = 2) of q_waves - 10.
+    int rb = force_q_waves >= 10 ? 2 : 1;
+    int qw = force_q_waves >= 10 ? force_q_waves - 10 : force_q_waves, kw = force_kv_waves;
+    if (!valid_shape(qw, kw, rb)) {
+        rb = 1;
         long blocks128 = 0;
         for (int i = 0; i < n; ++i) blocks128 += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 127) / 128);
         if (blocks128 >= 256) {
@@ -908,9 +1010,11 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
     }
     p.q_waves = qw;
     p.kv_waves = kw;
+    p.rows_per_wave = 32 * rb;
+    const int block_m = 32 * qw * rb;
     long groups = 0;
     for (int i = 0; i < n; ++i)
-        groups += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 32 * qw - 1) / (32 * qw));
+        groups += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + block_m - 1) / block_m);
     int want = force_splits > 0 ? force_splits : (int)std::max(1L, (256 + groups - 1) / std::max(1L, groups));
     want = std::max(1, std::min(want, kMaxSplits));
     for (;;) {
@@ -935,6 +1039,7 @@ LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves, int forc
     LaunchPlan p{};
     p.q_waves = g.q_waves;
     p.kv_waves = g.kv_waves;
+    p.rows_per_wave = g.rows_per_wave;
     p.splits = g.splits[0];
     p.tiles_per_split = g.tiles_per_split[0];
     p.ws_needed = g.ws_needed;
@@ -963,7 +1068,7 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
         ca.splits = p.splits[i];
         ca.tiles_per_split = p.tiles_per_split[i];
         ca.bh = c.batch * c.heads;
-        ca.qtiles = (c.nq + 32 * p.q_waves - 1) / (32 * p.q_waves);
+        ca.qtiles = (c.nq + 32 * p.q_waves * (p.rows_per_wave / 32) - 1) / (32 * p.q_waves * (p.rows_per_wave / 32));
         ca.block_begin = blocks;
         if (ca.splits > 1) {
             const size_t rows = (size_t)ca.bh * ca.splits * c.nq;
@@ -985,21 +1090,22 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
     if (n_live == 0) return hipSuccess;
     a.n_calls = n_live;
     a.total_blocks = blocks;
+    const int rbw = p.rows_per_wave / 32;
     hipError_t e = hipSuccess;
     if (phase_mask & 1) {
         if (in == InType::F16) {
-            e = (out == OutType::F16) ? launch_fwd_shape<f16, f16>(a, blocks, p.q_waves, p.kv_waves, stream)
-                                      : launch_fwd_shape<f16, float>(a, blocks, p.q_waves, p.kv_waves, stream);
+            e = (out == OutType::F16) ? launch_fwd_shape<f16, f16>(a, blocks, p.q_waves, p.kv_waves, rbw, stream)
+                                      : launch_fwd_shape<f16, float>(a, blocks, p.q_waves, p.kv_waves, rbw, stream);
         } else {
-            e = (out == OutType::F16) ? launch_fwd_shape<float, f16>(a, blocks, p.q_waves, p.kv_waves, stream)
-                                      : launch_fwd_shape<float, float>(a, blocks, p.q_waves, p.kv_waves, stream);
+            e = (out == OutType::F16) ? launch_fwd_shape<float, f16>(a, blocks, p.q_waves, p.kv_waves, rbw, stream)
+                                      : launch_fwd_shape<float, float>(a, blocks, p.q_waves, p.kv_waves, rbw, stream);
         }
     }
     if (e != hipSuccess || !any_split || !(phase_mask & 2)) return e;
     // Combine grid: for every XCD x, the groups (of calls that split) whose first split block
     // ran on x (same bijective order as the main kernel), 16 rows per block.
     cb.n_calls = n_live;
-    const int block_m = 32 * p.q_waves;
+    const int block_m = 32 * p.q_waves * rbw;
     cb.block_m_log2 = block_m == 32 ? 5 : (block_m == 64 ? 6 : 7);
     auto xb = [&](int xx) {
         const int q8 = blocks >> 3, r8 = blocks & 7;

@@ -369,7 +369,8 @@ int32_t mha_hd64_launch_forced(const void* q, const void* k, const void* v, void
     MHA_CHECK(nkv >= 1);
     const mha_hd64::Call c{q, k, v, o, batch, heads, nq, nkv};
     const mha_hd64::LaunchPlan plan = mha_hd64::plan_call(c, workspace ? ws_bytes : 0, q_waves, kv_waves, splits);
-    if (q_waves != 0 && (plan.q_waves != q_waves || plan.kv_waves != kv_waves))
+    const int plan_qw = plan.q_waves + (plan.rows_per_wave == 64 ? 10 : 0);
+    if (q_waves != 0 && (plan_qw != q_waves || plan.kv_waves != kv_waves))
         return fail(MHA_HD64_STATUS_BAD_PARAM, __FILE__, __LINE__, "forced workgroup shape is not compiled");
     if (splits > 1 && plan.splits != splits)
         return fail(MHA_HD64_STATUS_WORKSPACE, __FILE__, __LINE__, "forced split does not fit the workspace/keys");
@@ -388,7 +389,7 @@ size_t mha_hd64_plan(int32_t batch, int32_t heads, int32_t nq, int32_t nkv, size
     const mha_hd64::Call c{nullptr, nullptr, nullptr, nullptr, batch, heads, nq, nkv};
     const mha_hd64::LaunchPlan p = mha_hd64::plan_call(c, ws_bytes);
     if (out4) {
-        out4[0] = p.q_waves;
+        out4[0] = p.q_waves + (p.rows_per_wave == 64 ? 10 : 0);
         out4[1] = p.kv_waves;
         out4[2] = p.splits;
         out4[3] = p.tiles_per_split;

@@ -12,7 +12,8 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libmha_hd64.so")
+# MHA_HD64_LIB: test a diagnostic build (e.g. lib/exp/…) through the same suite.
+LIB_PATH = os.environ.get("MHA_HD64_LIB") or os.path.join(PKG_DIR, "lib", "libmha_hd64.so")
 
 DT_FLOAT = 0  # nvinfer1::DataType::kFLOAT
 DT_HALF = 1   # nvinfer1::DataType::kHALF

@@ -79,7 +79,7 @@ def test_fp16in_fp32out_launcher(name, dev):
 
 # ---- every launch plan (query-wave split x cross-workgroup KV split) against the C oracle ----
 PLAN_SHAPES = [(1, 1), (33, 65), (100, 100), (64, 2048), (300, 129), (1024, 1024), (257, 1000)]
-WG_SHAPES = [(4, 1), (2, 2), (1, 2), (4, 2)]
+WG_SHAPES = [(4, 1), (2, 2), (1, 2), (4, 2), (12, 2)]  # 12 = two 32-row query blocks per wave, 2 q-waves
 
 
 @pytest.mark.parametrize("nq,nkv", PLAN_SHAPES)
