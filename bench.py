@@ -277,6 +277,40 @@ def matcher_attention(torch, device, stream, rank, sizes=(512, 1024, 2048), laye
     return res
 
 
+def matcher_e2e(torch, device, stream, rank, sizes=(512, 1024, 2048), reps=10):
+    """BASELINE configs[3]: end-to-end LightGlue matcher latency (9 layers + final assignment,
+    fp16, seeded synthetic weights, N0 = N1 = N keypoints), one forward captured in a graph."""
+    from lightglue_amd import matcher
+
+    model = matcher.LightGlueMatcher(n_layers=9).eval()
+    model.load_state_dict(matcher.seeded_state_dict(7, 9), strict=True)
+    model = model.to(device, torch.float16)
+    res = {}
+    for n in sizes:
+        k0, k1, d0, d1 = (t.to(device, torch.float16) for t in matcher.synthetic_pair(40 + rank, n, n))
+        with torch.no_grad():
+            with torch.cuda.stream(stream):
+                for _ in range(2):
+                    model(k0, k1, d0, d1)          # warm: workspace + allocator outside the capture
+            stream.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream):
+                out = model(k0, k1, d0, d1)
+        g.replay()
+        stream.synchronize()
+        s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s_.record(stream)
+        with torch.cuda.stream(stream):
+            for _ in range(reps):
+                g.replay()
+        e_.record(stream)
+        stream.synchronize()
+        ms = s_.elapsed_time(e_) / reps
+        assert torch.isfinite(out[2]).all()
+        res[str(n)] = {"ms": round(ms, 4), "pairs_per_s": round(1e3 / ms, 1)}
+    return res
+
+
 def profile_driver(torch, args, device):
     """Eager launches of one workload (for rocprofv3 --kernel-trace / --pmc passes)."""
     import lightglue_amd
@@ -438,6 +472,7 @@ def main():
         }
 
         result["matcher_attention"] = matcher_attention(torch, device, stream, rank, separate=args.matcher_separate)
+        result["matcher_e2e_fp16"] = matcher_e2e(torch, device, stream, rank)
 
     if args.sweep and rank == 0:
         sweep(torch, lib, device, stream, nq, nkv)
