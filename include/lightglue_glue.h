@@ -1,0 +1,56 @@
+/*
+ * lightglue_glue.h — gfx950 kernels for the LightGlue matcher built around MHAHeadDim64
+ * (SURVEY.md section 8(f) ranks 3/4). Not part of the reference plugin's surface: these
+ * replace chains of small framework ops around the attention call in
+ * lightglue_pytorch_no_plugin/lightglue.py (one launch each instead of 3-8).
+ *
+ * Layouts are row-major and contiguous. dtype: MHA_HD64_DT_FLOAT (0) or MHA_HD64_DT_HALF (1)
+ * for every tensor argument of a call (statistics and softmax math in fp32). All calls are
+ * asynchronous on `stream` and return 0 or a nonzero status (message: mha_hd64_last_error()).
+ */
+#ifndef LIGHTGLUE_GLUE_H_
+#define LIGHTGLUE_GLUE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* SelfBlock q/k/v (lightglue.py:111-119, rotary :124-134): qkv [n0+n1, heads*64*3] is the Wqkv
+ * output with channel (h*64 + d)*3 + j; cos/sin [n0+n1, 64] the positional encoding (pairs
+ * repeated, lightglue.py:44-52). Writes q/k (rotated) and v of image i as [heads, ni, 64]. */
+int32_t lg_qkv_rotary_split(int32_t dtype, const void* qkv, const void* cos, const void* sin, int32_t heads,
+                            int32_t n0, int32_t n1, void* q0, void* k0, void* v0, void* q1, void* k1, void* v1,
+                            hipStream_t stream);
+
+/* CrossBlock heads (lightglue.py:158-166): a, b [n0+n1, heads*64] -> a0, b0 [heads, n0, 64],
+ * a1, b1 [heads, n1, 64]. */
+int32_t lg_split_heads2(int32_t dtype, const void* a, const void* b, int32_t heads, int32_t n0, int32_t n1,
+                        void* a0, void* a1, void* b0, void* b1, hipStream_t stream);
+
+/* Attention outputs back to rows (lightglue.py:118-120, 163-170): x0 [heads, n0, 64],
+ * x1 [heads, n1, 64] -> out [n0+n1, heads*64]. */
+int32_t lg_merge_heads(int32_t dtype, const void* x0, const void* x1, int32_t heads, int32_t n0, int32_t n1,
+                       void* out, hipStream_t stream);
+
+/* FFN middle (lightglue.py:101-106): y = GELU(LayerNorm(x) * gamma + beta), exact (erf) GELU,
+ * x, y [rows, dim], dim a multiple of 64 and <= 1024. */
+int32_t lg_layernorm_gelu(int32_t dtype, const void* x, const void* gamma, const void* beta, int32_t rows,
+                          int32_t dim, float eps, void* y, hipStream_t stream);
+
+/* sigmoid_log_double_softmax (lightglue.py:197-205), fp32: scores[i][j] = 2 sim[i][j]
+ * - logsumexp_j' sim[i][j'] - logsumexp_i' sim[i'][j] + logsigmoid(z0[i]) + logsigmoid(z1[j]).
+ * sim, scores [m, n]; z0 [m], z1 [n]; workspace >= lg_log_double_softmax_workspace(m, n) bytes. */
+size_t lg_log_double_softmax_workspace(int32_t m, int32_t n);
+int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1, int32_t m, int32_t n,
+                              float* scores, void* workspace, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LIGHTGLUE_GLUE_H_ */

@@ -1,0 +1,288 @@
+// lightglue_glue.hip — gfx950 kernels for the matcher around MHAHeadDim64 (include/lightglue_glue.h).
+//
+// Memory-bound layout/normalisation kernels: one pass over the data each, 16-B accesses where the
+// layout allows, one wave64 per row for row statistics (shuffle-xor reductions), fp32 math.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "lightglue_glue.h"
+#include "mha_hd64.h"
+#include "mha_hd64_internal.h"
+
+namespace {
+
+typedef _Float16 f16;
+
+template <typename T> __device__ __forceinline__ float ld(const T* p) { return (float)*p; }
+template <typename T> __device__ __forceinline__ void st(T* p, float v) { *p = (T)v; }
+
+constexpr int kD = 64;  // head dim
+
+// ---- q/k/v split + rotary (thread = one (row, head, rotary pair)) ----
+template <typename T>
+__global__ __launch_bounds__(256) void qkv_rotary_split_kernel(const T* __restrict__ qkv, const T* __restrict__ cosv,
+                                                               const T* __restrict__ sinv, int heads, int n0, int n1,
+                                                               T* q0, T* k0, T* v0, T* q1, T* k1, T* v1) {
+    const int ntot = n0 + n1;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long)ntot * heads * (kD / 2)) return;
+    const int p = idx % (kD / 2);
+    const int h = (idx / (kD / 2)) % heads;
+    const int n = idx / ((long)(kD / 2) * heads);
+    // channels (h*64 + 2p + t)*3 + j, t in {0,1}, j in {q,k,v}: six consecutive values
+    const T* src = qkv + (size_t)n * heads * kD * 3 + (size_t)(h * kD + 2 * p) * 3;
+    const float q_a = ld(src + 0), k_a = ld(src + 1), v_a = ld(src + 2);
+    const float q_b = ld(src + 3), k_b = ld(src + 4), v_b = ld(src + 5);
+    const float c = ld(cosv + (size_t)n * kD + 2 * p), s = ld(sinv + (size_t)n * kD + 2 * p);
+    const bool first = n < n0;
+    const int row = first ? n : n - n0, nn = first ? n0 : n1;
+    const size_t o = ((size_t)h * nn + row) * kD + 2 * p;
+    T* qd = first ? q0 : q1;
+    T* kd = first ? k0 : k1;
+    T* vd = first ? v0 : v1;
+    // (x0, x1) -> (x0 c - x1 s, x1 c + x0 s)   (t*cos + rotate_half(t)*sin)
+    st(qd + o, q_a * c - q_b * s);
+    st(qd + o + 1, q_b * c + q_a * s);
+    st(kd + o, k_a * c - k_b * s);
+    st(kd + o + 1, k_b * c + k_a * s);
+    st(vd + o, v_a);
+    st(vd + o + 1, v_b);
+}
+
+// 16-B vector of T
+template <typename T> struct V16;
+template <> struct V16<f16> { typedef unsigned int type __attribute__((ext_vector_type(4))); static constexpr int n = 8; };
+template <> struct V16<float> { typedef unsigned int type __attribute__((ext_vector_type(4))); static constexpr int n = 4; };
+
+// ---- [rows, heads*64] <-> per image [heads, ni, 64] (thread = one 16-B chunk) ----
+template <typename T, bool SPLIT>
+__global__ __launch_bounds__(256) void heads_kernel(const T* a, const T* b, T* a0, T* a1, T* b0, T* b1, int heads,
+                                                    int n0, int n1) {
+    typedef typename V16<T>::type vec;
+    constexpr int E = V16<T>::n;
+    constexpr int CH = kD / E;  // chunks per head row
+    const int ntot = n0 + n1;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long per = (long)ntot * heads * CH;
+    if (idx >= (b ? 2 : 1) * per) return;
+    const bool second = idx >= per;
+    const long i = second ? idx - per : idx;
+    const int c = i % CH;
+    const int h = (i / CH) % heads;
+    const int n = i / ((long)CH * heads);
+    const bool first = n < n0;
+    const int row = first ? n : n - n0, nn = first ? n0 : n1;
+    const size_t rows_off = (size_t)n * heads * kD + h * kD + c * E;
+    const size_t head_off = ((size_t)h * nn + row) * kD + c * E;
+    if (SPLIT) {
+        const T* src = second ? b : a;
+        T* dst = second ? (first ? b0 : b1) : (first ? a0 : a1);
+        *reinterpret_cast<vec*>(dst + head_off) = *reinterpret_cast<const vec*>(src + rows_off);
+    } else {  // merge: a = x0, b = x1 (head-major inputs), a0 = out
+        const T* src = first ? a : b;
+        *reinterpret_cast<vec*>(a0 + rows_off) = *reinterpret_cast<const vec*>(src + head_off);
+    }
+}
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+    return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) x = fmaxf(x, __shfl_xor(x, m, 64));
+    return x;
+}
+
+// ---- LayerNorm + exact GELU (one wave per row, dim / 64 values per lane) ----
+template <typename T, int PER>
+__global__ __launch_bounds__(256) void ln_gelu_kernel(const T* __restrict__ x, const T* __restrict__ g,
+                                                      const T* __restrict__ bta, int rows, float eps, T* y) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    constexpr int dim = PER * 64;
+    const T* xr = x + (size_t)row * dim;
+    float v[PER];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        v[i] = ld(xr + i * 64 + lane);
+        s += v[i];
+    }
+    const float mean = wave_sum(s) * (1.f / dim);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        v[i] -= mean;
+        q += v[i] * v[i];
+    }
+    const float rstd = rsqrtf(wave_sum(q) * (1.f / dim) + eps);
+    T* yr = y + (size_t)row * dim;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int c = i * 64 + lane;
+        const float t = v[i] * rstd * ld(g + c) + ld(bta + c);
+        st(yr + c, 0.5f * t * (1.f + erff(t * 0.70710678118654752f)));
+    }
+}
+
+// ---- dual log-softmax ----
+// pass 1: blocks [0, rb) -> row logsumexp (one wave per row); blocks [rb, ...) -> column
+// logsumexp (one thread per column, online max/sum down the rows; consecutive threads read
+// consecutive columns of a row: coalesced).
+__global__ __launch_bounds__(256) void lse_kernel(const float* __restrict__ sim, int m, int n, int rb,
+                                                  float* lse_row, float* lse_col) {
+    if ((int)blockIdx.x < rb) {
+        const int lane = threadIdx.x & 63;
+        const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+        if (row >= m) return;
+        const float* r = sim + (size_t)row * n;
+        float mx = -INFINITY;
+        for (int j = lane; j < n; j += 64) mx = fmaxf(mx, r[j]);
+        mx = wave_max(mx);
+        float s = 0.f;
+        for (int j = lane; j < n; j += 64) s += __expf(r[j] - mx);
+        s = wave_sum(s);
+        if (lane == 0) lse_row[row] = mx + __logf(s);
+    } else {
+        const int col = (blockIdx.x - rb) * blockDim.x + threadIdx.x;
+        if (col >= n) return;
+        float mx = -INFINITY, s = 0.f;
+        for (int i = 0; i < m; ++i) {
+            const float v = sim[(size_t)i * n + col];
+            if (v > mx) {
+                s = s * __expf(mx - v) + 1.f;
+                mx = v;
+            } else {
+                s += __expf(v - mx);
+            }
+        }
+        lse_col[col] = mx + __logf(s);
+    }
+}
+
+__device__ __forceinline__ float log_sigmoid(float z) { return fminf(z, 0.f) - log1pf(__expf(-fabsf(z))); }
+
+// pass 2: scores = 2 sim - lse_row[i] - lse_col[j] + logsig(z0[i]) + logsig(z1[j])
+__global__ __launch_bounds__(256) void dual_combine_kernel(const float* __restrict__ sim, const float* z0,
+                                                           const float* z1, const float* lse_row,
+                                                           const float* lse_col, int m, int n, float* out) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long)m * n) return;
+    const int i = idx / n, j = idx - (long)i * n;
+    out[idx] = 2.f * sim[idx] - lse_row[i] - lse_col[j] + log_sigmoid(z0[i]) + log_sigmoid(z1[j]);
+}
+
+inline unsigned blocks_for(long threads) { return (unsigned)((threads + 255) / 256); }
+
+int32_t launched(const char* what) {
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return MHA_HD64_STATUS_SUCCESS;
+    return mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, what, hipGetErrorString(e));
+}
+
+bool bad_dtype(int32_t dt) { return dt != MHA_HD64_DT_HALF && dt != MHA_HD64_DT_FLOAT; }
+
+}  // namespace
+
+extern "C" {
+
+int32_t lg_qkv_rotary_split(int32_t dtype, const void* qkv, const void* cosv, const void* sinv, int32_t heads,
+                            int32_t n0, int32_t n1, void* q0, void* k0, void* v0, void* q1, void* k1, void* v1,
+                            hipStream_t stream) {
+    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || !qkv || !cosv || !sinv)
+        return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_qkv_rotary_split", "bad arguments");
+    const long threads = (long)(n0 + n1) * heads * (kD / 2);
+    if (threads == 0) return MHA_HD64_STATUS_SUCCESS;
+    if (dtype == MHA_HD64_DT_HALF)
+        hipLaunchKernelGGL(qkv_rotary_split_kernel<f16>, dim3(blocks_for(threads)), dim3(256), 0, stream,
+                           (const f16*)qkv, (const f16*)cosv, (const f16*)sinv, heads, n0, n1, (f16*)q0, (f16*)k0,
+                           (f16*)v0, (f16*)q1, (f16*)k1, (f16*)v1);
+    else
+        hipLaunchKernelGGL(qkv_rotary_split_kernel<float>, dim3(blocks_for(threads)), dim3(256), 0, stream,
+                           (const float*)qkv, (const float*)cosv, (const float*)sinv, heads, n0, n1, (float*)q0,
+                           (float*)k0, (float*)v0, (float*)q1, (float*)k1, (float*)v1);
+    return launched("lg_qkv_rotary_split");
+}
+
+int32_t lg_split_heads2(int32_t dtype, const void* a, const void* b, int32_t heads, int32_t n0, int32_t n1,
+                        void* a0, void* a1, void* b0, void* b1, hipStream_t stream) {
+    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || !a)
+        return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_split_heads2", "bad arguments");
+    const int E = dtype == MHA_HD64_DT_HALF ? 8 : 4;
+    const long threads = (b ? 2 : 1) * (long)(n0 + n1) * heads * (kD / E);
+    if (threads == 0) return MHA_HD64_STATUS_SUCCESS;
+    if (dtype == MHA_HD64_DT_HALF)
+        hipLaunchKernelGGL((heads_kernel<f16, true>), dim3(blocks_for(threads)), dim3(256), 0, stream, (const f16*)a,
+                           (const f16*)b, (f16*)a0, (f16*)a1, (f16*)b0, (f16*)b1, heads, n0, n1);
+    else
+        hipLaunchKernelGGL((heads_kernel<float, true>), dim3(blocks_for(threads)), dim3(256), 0, stream,
+                           (const float*)a, (const float*)b, (float*)a0, (float*)a1, (float*)b0, (float*)b1, heads,
+                           n0, n1);
+    return launched("lg_split_heads2");
+}
+
+int32_t lg_merge_heads(int32_t dtype, const void* x0, const void* x1, int32_t heads, int32_t n0, int32_t n1,
+                       void* out, hipStream_t stream) {
+    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || !out)
+        return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_merge_heads", "bad arguments");
+    const int E = dtype == MHA_HD64_DT_HALF ? 8 : 4;
+    const long threads = (long)(n0 + n1) * heads * (kD / E);
+    if (threads == 0) return MHA_HD64_STATUS_SUCCESS;
+    if (dtype == MHA_HD64_DT_HALF)
+        hipLaunchKernelGGL((heads_kernel<f16, false>), dim3(blocks_for(threads)), dim3(256), 0, stream,
+                           (const f16*)x0, (const f16*)x1, (f16*)out, nullptr, nullptr, nullptr, heads, n0, n1);
+    else
+        hipLaunchKernelGGL((heads_kernel<float, false>), dim3(blocks_for(threads)), dim3(256), 0, stream,
+                           (const float*)x0, (const float*)x1, (float*)out, nullptr, nullptr, nullptr, heads, n0,
+                           n1);
+    return launched("lg_merge_heads");
+}
+
+int32_t lg_layernorm_gelu(int32_t dtype, const void* x, const void* gamma, const void* beta, int32_t rows,
+                          int32_t dim, float eps, void* y, hipStream_t stream) {
+    if (bad_dtype(dtype) || rows < 0 || dim <= 0 || dim % 64 != 0 || dim > 1024 || !x || !gamma || !beta || !y)
+        return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_layernorm_gelu", "bad arguments");
+    if (rows == 0) return MHA_HD64_STATUS_SUCCESS;
+    const dim3 grid((rows + 3) / 4);
+#define LG_LN(PER)                                                                                              \
+    case PER:                                                                                                   \
+        if (dtype == MHA_HD64_DT_HALF)                                                                          \
+            hipLaunchKernelGGL((ln_gelu_kernel<f16, PER>), grid, dim3(256), 0, stream, (const f16*)x,           \
+                               (const f16*)gamma, (const f16*)beta, rows, eps, (f16*)y);                        \
+        else                                                                                                    \
+            hipLaunchKernelGGL((ln_gelu_kernel<float, PER>), grid, dim3(256), 0, stream, (const float*)x,       \
+                               (const float*)gamma, (const float*)beta, rows, eps, (float*)y);                  \
+        break;
+    switch (dim / 64) {
+        LG_LN(1) LG_LN(2) LG_LN(4) LG_LN(8) LG_LN(16)
+        default:
+            return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_layernorm_gelu",
+                                          "dim must be 64, 128, 256, 512 or 1024");
+    }
+#undef LG_LN
+    return launched("lg_layernorm_gelu");
+}
+
+size_t lg_log_double_softmax_workspace(int32_t m, int32_t n) {
+    return (size_t)((m > 0 ? m : 0) + (n > 0 ? n : 0)) * sizeof(float);
+}
+
+int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1, int32_t m, int32_t n, float* scores,
+                              void* workspace, hipStream_t stream) {
+    if (m < 0 || n < 0 || ((m > 0 && n > 0) && (!sim || !z0 || !z1 || !scores || !workspace)))
+        return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_log_double_softmax", "bad arguments");
+    if (m == 0 || n == 0) return MHA_HD64_STATUS_SUCCESS;
+    float* lse_row = reinterpret_cast<float*>(workspace);
+    float* lse_col = lse_row + m;
+    const int rb = (m + 3) / 4;
+    hipLaunchKernelGGL(lse_kernel, dim3(rb + blocks_for(n)), dim3(256), 0, stream, sim, m, n, rb, lse_row, lse_col);
+    hipLaunchKernelGGL(dual_combine_kernel, dim3(blocks_for((long)m * n)), dim3(256), 0, stream, sim, z0, z1, lse_row,
+                       lse_col, m, n, scores);
+    return launched("lg_log_double_softmax");
+}
+
+}  // extern "C"

@@ -71,6 +71,9 @@ hipError_t launch_attention(const Call& c, InType in, OutType out, void* workspa
                             hipStream_t stream, int force_q_waves = 0, int force_kv_waves = 0,
                             int force_splits = 0, int phase_mask = 3);
 
+// Record an error for mha_hd64_last_error() (and abort if abort-on-error is set); returns status.
+int32_t report_error(int32_t status, const char* where, const char* what);
+
 // Diagnostic builds (-DMHA_STAMPS): where the kernel writes its per-workgroup timestamps.
 void set_stamp_buffer(void* p);
 

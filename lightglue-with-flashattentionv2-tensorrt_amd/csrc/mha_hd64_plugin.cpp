@@ -398,3 +398,11 @@ size_t mha_hd64_plan(int32_t batch, int32_t heads, int32_t nq, int32_t nkv, size
 }
 
 }  // extern "C"
+
+namespace mha_hd64 {
+int32_t report_error(int32_t status, const char* where, const char* what) {
+    char buf[256];
+    std::snprintf(buf, sizeof(buf), "%s: %s", where, what);
+    return fail(status, __FILE__, __LINE__, buf);
+}
+}  // namespace mha_hd64

@@ -119,6 +119,16 @@ SIGNATURES = {
     "mha_hd64_set_abort_on_error": ([_I], None),
     "mha_hd64_build_info": ([], _C),
 }
+# include/lightglue_glue.h (matcher kernels around the op)
+_F = ctypes.POINTER(ctypes.c_float)
+SIGNATURES.update({
+    "lg_qkv_rotary_split": ([_I, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P], _I),
+    "lg_split_heads2": ([_I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P], _I),
+    "lg_merge_heads": ([_I, _P, _P, _I, _I, _I, _P, _P], _I),
+    "lg_layernorm_gelu": ([_I, _P, _P, _P, _I, _I, ctypes.c_float, _P, _P], _I),
+    "lg_log_double_softmax_workspace": ([_I, _I], _S),
+    "lg_log_double_softmax": ([_P, _P, _P, _I, _I, _P, _P, _P], _I),
+})
 # Test/bench hooks exported by the library but not part of the public header.
 HOOKS = {
     "mha_hd64_launch_forced": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _S, _P, _I], _I),

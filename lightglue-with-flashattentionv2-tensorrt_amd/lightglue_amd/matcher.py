@@ -16,6 +16,10 @@ What is different, and why:
   in one copy (the reference splits an interleaved [N, H, 64, 3] projection and transposes);
 * the column log-softmax of the assignment runs on a contiguous transpose (the reference's
   strided ``log_softmax(sim, 1)``);
+* ``glue="hip"`` (default) runs the layout/normalisation steps around the attention on gfx950
+  kernels (include/lightglue_glue.h: q/k/v split + rotary + per-image head-major layout in one
+  pass, head split/merge, LayerNorm+GELU, the dual log-softmax); ``glue="torch"`` is the same
+  math in framework ops (the restatement the CPU tests pin to the reference);
 * ``attention=`` lets tests substitute the oracle for the kernel on CPU; the default path
   requires GPU tensors and fails loudly otherwise (no CPU fallback).
 """
@@ -29,10 +33,79 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from . import synth
-from .plugin import PluginError, mha_hd64_grouped
+from . import _lib, synth
+from .plugin import PluginError, _check, _workspace, mha_hd64_grouped
 
 AttnFn = Callable[[Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]], List[torch.Tensor]]
+
+
+_DT = {torch.float16: _lib.DT_HALF, torch.float32: _lib.DT_FLOAT}
+
+
+class _Hip:
+    """Thin wrappers of the gfx950 glue kernels (current stream, fail loudly on error)."""
+
+    @staticmethod
+    def _stream(t):
+        return torch.cuda.current_stream(t.device).cuda_stream
+
+    @staticmethod
+    def qkv_rotary_split(qkv, cos, sin, heads, splits):
+        n0, n1 = splits
+        mk = lambda n: torch.empty((1, heads, n, 64), dtype=qkv.dtype, device=qkv.device)  # noqa: E731
+        out = [tuple(mk(n) for _ in range(3)) for n in (n0, n1)]
+        st = _lib.load().lg_qkv_rotary_split(_DT[qkv.dtype], qkv.data_ptr(), cos.data_ptr(), sin.data_ptr(), heads,
+                                             n0, n1, *(t.data_ptr() for t in out[0]),
+                                             *(t.data_ptr() for t in out[1]), _Hip._stream(qkv))
+        _check(st, "lg_qkv_rotary_split")
+        return out
+
+    @staticmethod
+    def split_heads2(a, b, heads, splits):
+        n0, n1 = splits
+        mk = lambda n: torch.empty((1, heads, n, 64), dtype=a.dtype, device=a.device)  # noqa: E731
+        a0, a1, b0, b1 = mk(n0), mk(n1), mk(n0), mk(n1)
+        st = _lib.load().lg_split_heads2(_DT[a.dtype], a.data_ptr(), b.data_ptr(), heads, n0, n1, a0.data_ptr(),
+                                         a1.data_ptr(), b0.data_ptr(), b1.data_ptr(), _Hip._stream(a))
+        _check(st, "lg_split_heads2")
+        return (a0, a1), (b0, b1)
+
+    @staticmethod
+    def merge_heads(x0, x1):
+        heads, n0, n1 = x0.shape[1], x0.shape[2], x1.shape[2]
+        out = torch.empty((1, n0 + n1, heads * 64), dtype=x0.dtype, device=x0.device)
+        st = _lib.load().lg_merge_heads(_DT[x0.dtype], x0.data_ptr(), x1.data_ptr(), heads, n0, n1, out.data_ptr(),
+                                        _Hip._stream(x0))
+        _check(st, "lg_merge_heads")
+        return out
+
+    @staticmethod
+    def layernorm_gelu(x, ln: nn.LayerNorm):
+        y = torch.empty_like(x)
+        rows, dim = x.numel() // x.shape[-1], x.shape[-1]
+        st = _lib.load().lg_layernorm_gelu(_DT[x.dtype], x.data_ptr(), ln.weight.data_ptr(), ln.bias.data_ptr(), rows,
+                                           dim, float(ln.eps), y.data_ptr(), _Hip._stream(x))
+        _check(st, "lg_layernorm_gelu")
+        return y
+
+    @staticmethod
+    def log_double_softmax(sim, z0, z1):
+        m, n = sim.shape[1], sim.shape[2]
+        lib = _lib.load()
+        out = torch.empty_like(sim)
+        stream = _Hip._stream(sim)
+        ws = _workspace(sim.device, stream, lib.lg_log_double_softmax_workspace(m, n))
+        st = lib.lg_log_double_softmax(sim.data_ptr(), z0.data_ptr(), z1.data_ptr(), m, n, out.data_ptr(),
+                                       ws.data_ptr(), stream)
+        _check(st, "lg_log_double_softmax")
+        return out
+
+
+def _ffn_apply(ffn: nn.Sequential, h: torch.Tensor, hip: bool) -> torch.Tensor:
+    """Linear -> LayerNorm -> GELU -> Linear (the LN+GELU pair is one gfx950 kernel on the hip path)."""
+    if not hip:
+        return ffn(h)
+    return ffn[3](_Hip.layernorm_gelu(ffn[0](h), ffn[1]))
 
 
 def _kernel_attention(calls):
@@ -80,9 +153,11 @@ class SelfBlock(nn.Module):
         self.out_proj = nn.Linear(d, d)
         self.ffn = _ffn(d)
 
-    def qkv(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, splits: Sequence[int]):
+    def qkv(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, splits: Sequence[int], hip: bool = False):
         """x [1, N0+N1, d] (both images' rows) -> per image (q, k, v), each [1, H, Ni, 64]."""
         n = x.shape[1]
+        if hip:
+            return _Hip.qkv_rotary_split(self.Wqkv(x), cos, sin, self.heads, splits)
         # Wqkv output channel (h*64 + d)*3 + j  ->  [3, H, N, 64] head-major
         t = self.Wqkv(x).view(n, self.heads, self.head_dim, 3).permute(3, 1, 0, 2)
         q = _rotary(t[0], cos, sin)
@@ -93,9 +168,12 @@ class SelfBlock(nn.Module):
             a += ni
         return out
 
-    def finish(self, x: torch.Tensor, contexts: Sequence[torch.Tensor]) -> torch.Tensor:
-        msg = self.out_proj(torch.cat([c[0].transpose(0, 1).reshape(c.shape[2], -1) for c in contexts], 0)[None])
-        return x + self.ffn(torch.cat((x, msg), -1))
+    def finish(self, x: torch.Tensor, contexts: Sequence[torch.Tensor], hip: bool = False) -> torch.Tensor:
+        if hip:
+            merged = _Hip.merge_heads(*contexts)
+        else:
+            merged = torch.cat([c[0].transpose(0, 1).reshape(c.shape[2], -1) for c in contexts], 0)[None]
+        return x + _ffn_apply(self.ffn, torch.cat((x, self.out_proj(merged)), -1), hip)
 
 
 class CrossBlock(nn.Module):
@@ -118,9 +196,12 @@ class CrossBlock(nn.Module):
             a += ni
         return out
 
-    def finish(self, x: torch.Tensor, ms: Sequence[torch.Tensor]) -> torch.Tensor:
-        msg = self.to_out(torch.cat([m[0].transpose(0, 1).reshape(m.shape[2], -1) for m in ms], 0)[None])
-        return x + self.ffn(torch.cat((x, msg), -1))
+    def finish(self, x: torch.Tensor, ms: Sequence[torch.Tensor], hip: bool = False) -> torch.Tensor:
+        if hip:
+            merged = _Hip.merge_heads(*ms)
+        else:
+            merged = torch.cat([m[0].transpose(0, 1).reshape(m.shape[2], -1) for m in ms], 0)[None]
+        return x + _ffn_apply(self.ffn, torch.cat((x, self.to_out(merged)), -1), hip)
 
 
 class TransformerLayer(nn.Module):
@@ -129,13 +210,16 @@ class TransformerLayer(nn.Module):
         self.self_attn = SelfBlock(d, heads)
         self.cross_attn = CrossBlock(d, heads)
 
-    def forward(self, x, cos, sin, splits, attention: AttnFn):
+    def forward(self, x, cos, sin, splits, attention: AttnFn, hip: bool = False):
         """x: both images' descriptors [1, N0+N1, d] (image 0 rows first)."""
         sa, ca = self.self_attn, self.cross_attn
-        x = sa.finish(x, attention(sa.qkv(x, cos, sin, splits)))       # one grouped launch (self0, self1)
-        qk0, qk1 = ca.heads_of(ca.to_qk(x), splits)
-        v0, v1 = ca.heads_of(ca.to_v(x), splits)
-        return ca.finish(x, attention([(qk0, qk1, v1), (qk1, qk0, v0)]))  # one grouped launch (cross)
+        x = sa.finish(x, attention(sa.qkv(x, cos, sin, splits, hip)), hip)   # one grouped launch (self0, self1)
+        if hip:
+            (qk0, qk1), (v0, v1) = _Hip.split_heads2(ca.to_qk(x), ca.to_v(x), ca.heads, splits)
+        else:
+            qk0, qk1 = ca.heads_of(ca.to_qk(x), splits)
+            v0, v1 = ca.heads_of(ca.to_v(x), splits)
+        return ca.finish(x, attention([(qk0, qk1, v1), (qk1, qk0, v0)]), hip)  # one grouped launch (cross)
 
 
 def log_double_softmax(sim: torch.Tensor, z0: torch.Tensor, z1: torch.Tensor) -> torch.Tensor:
@@ -154,11 +238,14 @@ class MatchAssignment(nn.Module):
         self.final_proj = nn.Linear(d, d)
         self.matchability = nn.Linear(d, 1)
 
-    def forward(self, d0: torch.Tensor, d1: torch.Tensor) -> torch.Tensor:
+    def forward(self, d0: torch.Tensor, d1: torch.Tensor, hip: bool = False) -> torch.Tensor:
         m0 = self.final_proj(d0) / self.scale
         m1 = self.final_proj(d1) / self.scale
-        sim = m0 @ m1.transpose(1, 2)
-        return log_double_softmax(sim.float(), self.matchability(d0).float(), self.matchability(d1).float())
+        sim = (m0 @ m1.transpose(1, 2)).float()
+        z0, z1 = self.matchability(d0).float(), self.matchability(d1).float()
+        if hip:
+            return _Hip.log_double_softmax(sim.contiguous(), z0.contiguous(), z1.contiguous())
+        return log_double_softmax(sim, z0, z1)
 
 
 def filter_matches(scores: torch.Tensor, th: float):
@@ -181,7 +268,7 @@ class LightGlueMatcher(nn.Module):
         -> (desc0 [1,M,d], desc1 [1,N,d], log-assignment scores [1,M,N] fp32)"""
 
     def __init__(self, n_layers: int = 9, descriptor_dim: int = 256, input_dim: int = 256, num_heads: int = 4,
-                 filter_threshold: float = 0.1, attention: Optional[AttnFn] = None) -> None:
+                 filter_threshold: float = 0.1, attention: Optional[AttnFn] = None, glue: str = "hip") -> None:
         super().__init__()
         d = descriptor_dim
         self.n_layers, self.filter_threshold = n_layers, filter_threshold
@@ -190,16 +277,24 @@ class LightGlueMatcher(nn.Module):
         self.transformers = nn.ModuleList([TransformerLayer(d, num_heads) for _ in range(n_layers)])
         self.log_assignment = nn.ModuleList([MatchAssignment(d) for _ in range(n_layers)])
         self.attention = attention or _kernel_attention
+        if glue not in ("hip", "torch"):
+            raise ValueError("glue must be 'hip' or 'torch'")
+        self.glue = glue
 
     def forward(self, kpts0, kpts1, desc0, desc1):
         splits = (desc0.shape[1], desc1.shape[1])
         x = self.input_proj(torch.cat((desc0, desc1), 1))
+        hip = self.glue == "hip"
+        if hip and not x.is_cuda:
+            raise PluginError("LightGlueMatcher(glue='hip') runs on the GPU only (no CPU fallback)")
         cos, sin = self.posenc(torch.cat((kpts0, kpts1), 1).to(x.dtype))
         cos, sin = cos[0], sin[0]                                  # [1, N0+N1, 64], broadcast over heads
+        if hip:
+            cos, sin = cos.contiguous(), sin.contiguous()
         for layer in self.transformers:
-            x = layer(x, cos, sin, splits, self.attention)
+            x = layer(x, cos, sin, splits, self.attention, hip)
         d0, d1 = x[:, :splits[0]], x[:, splits[0]:]
-        return d0, d1, self.log_assignment[self.n_layers - 1](d0, d1)
+        return d0, d1, self.log_assignment[self.n_layers - 1](d0, d1, hip)
 
     def match(self, kpts0, kpts1, desc0, desc1):
         """forward + filter_matches (the demo's post-processing)."""

@@ -10,13 +10,15 @@ import pytest
 
 from conftest import REPO
 
-HEADER = os.path.join(REPO, "include", "mha_hd64.h")
+HEADERS = [os.path.join(REPO, "include", h) for h in ("mha_hd64.h", "lightglue_glue.h")]
 
 
 def header_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(mha_hd64_[a-z0-9_]+)\s*\(", src)))
+    names = set()
+    for h in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b((?:mha_hd64|lg)_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 @pytest.fixture(scope="module")
@@ -56,7 +58,7 @@ def test_every_header_symbol_is_exported(lib):
         assert hasattr(lib, n), n
         assert n in _lib.SIGNATURES, f"{n} has no ctypes signature"
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
-    exported = set(re.findall(r" T (mha_hd64_\w+)", out))
+    exported = set(re.findall(r" T ((?:mha_hd64|lg)_\w+)", out))
     assert set(names) <= exported
 
 

@@ -34,11 +34,11 @@ TOL_DESC16, TOL_SCORE16 = 1e-1, 0.6
 MATCH_RECALL = 0.9
 
 
-def _model(name, attention=None):
+def _model(name, attention=None, glue="hip"):
     from lightglue_amd import matcher
 
     meta = INDEX[name]
-    m = matcher.LightGlueMatcher(n_layers=meta["n_layers"], attention=attention).eval()
+    m = matcher.LightGlueMatcher(n_layers=meta["n_layers"], attention=attention, glue=glue).eval()
     sd = matcher.seeded_state_dict(meta["seed"], meta["n_layers"])
     m.load_state_dict(sd, strict=True)
     pair = matcher.synthetic_pair(meta["seed"], meta["m"], meta["n"])
@@ -72,7 +72,7 @@ def test_seeded_inputs_reproduce(name):
 @pytest.mark.parametrize("name", CASES)
 def test_cpu_restatement_matches_reference(name):
     g = np.load(os.path.join(GOLD, f"{name}.npz"))
-    model, _, pair = _model(name, attention=_oracle_attention)
+    model, _, pair = _model(name, attention=_oracle_attention, glue="torch")
     with torch.no_grad():
         d0, d1, sc = model(*pair)
     assert float((d0 - torch.from_numpy(g["desc0"])).abs().max()) <= TOL_CPU
@@ -94,17 +94,18 @@ def test_filter_matches_restatement(name):
             assert abs(ref_scores[(a, b)] - v) <= 1e-6
 
 
-def test_default_attention_refuses_cpu():
+@pytest.mark.parametrize("glue", ["hip", "torch"])
+def test_default_attention_refuses_cpu(glue):
     from lightglue_amd import PluginError
 
-    model, _, pair = _model(CASES[0])
+    model, _, pair = _model(CASES[0], glue=glue)
     with pytest.raises(PluginError):
         with torch.no_grad():
             model(*pair)
 
 
-def _gpu_run(name, dtype):
-    model, _, pair = _model(name)
+def _gpu_run(name, dtype, glue="hip"):
+    model, _, pair = _model(name, glue=glue)
     dev = torch.device("cuda:0")
     model = model.to(dev, dtype)
     with torch.no_grad():
@@ -116,15 +117,16 @@ def _gpu_run(name, dtype):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("glue", ["hip", "torch"])
 @pytest.mark.parametrize("dtype,tol_d,tol_s", [("float32", TOL_DESC32, TOL_SCORE32),
                                                ("float16", TOL_DESC16, TOL_SCORE16)])
-def test_gpu_matcher_matches_reference(name, dtype, tol_d, tol_s):
+def test_gpu_matcher_matches_reference(name, glue, dtype, tol_d, tol_s):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from lightglue_amd.matcher import filter_matches
 
     g = np.load(os.path.join(GOLD, f"{name}.npz"))
-    _, d0, d1, sc = _gpu_run(name, getattr(torch, dtype))
+    _, d0, d1, sc = _gpu_run(name, getattr(torch, dtype), glue)
     assert torch.isfinite(sc).all()
     assert float((d0 - torch.from_numpy(g["desc0"])).abs().max()) <= tol_d
     assert float((d1 - torch.from_numpy(g["desc1"])).abs().max()) <= tol_d
@@ -132,3 +134,51 @@ def test_gpu_matcher_matches_reference(name, dtype, tol_d, tol_s):
     got = _match_set(filter_matches(sc, 0.0)[0].numpy())
     ref = _match_set(g["matches_all"])
     assert len(got & ref) >= MATCH_RECALL * len(ref)
+
+
+# ---- the glue kernels one by one against the torch restatement (include/lightglue_glue.h) ----
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["float32", "float16"])
+def test_glue_kernels_match_torch(dtype):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lightglue_amd import matcher as mt
+
+    dt = getattr(torch, dtype)
+    dev = torch.device("cuda:0")
+    gen = torch.Generator().manual_seed(3)
+    rnd = lambda *s: torch.randn(*s, generator=gen).to(dev, dt)  # noqa: E731
+    tol = 2e-3 if dtype == "float16" else 1e-5
+    n0, n1, h = 37, 70, 4
+    blk = mt.SelfBlock(256, h).to(dev, dt)
+    x = rnd(1, n0 + n1, 256)
+    ang = rnd(1, n0 + n1, 32).float()
+    cos = torch.cos(ang).repeat_interleave(2, -1).to(dt)
+    sin = torch.sin(ang).repeat_interleave(2, -1).to(dt)
+    with torch.no_grad():
+        ref = blk.qkv(x, cos, sin, (n0, n1), hip=False)
+        got = blk.qkv(x, cos.contiguous(), sin.contiguous(), (n0, n1), hip=True)
+        for r3, g3 in zip(ref, got):
+            for r, g_ in zip(r3, g3):
+                assert float((r.float() - g_.float()).abs().max()) <= tol * 4
+        a, b = rnd(1, n0 + n1, 256), rnd(1, n0 + n1, 256)
+        cb = mt.CrossBlock(256, h)
+        (a0, a1), (b0, b1) = mt._Hip.split_heads2(a, b, h, (n0, n1))
+        for r, g_ in zip(cb.heads_of(a, (n0, n1)) + cb.heads_of(b, (n0, n1)), (a0, a1, b0, b1)):
+            assert torch.equal(r, g_)
+        merged = mt._Hip.merge_heads(a0, a1)
+        assert torch.equal(merged, a)
+        ln = torch.nn.LayerNorm(512).to(dev, dt)
+        with torch.no_grad():
+            ln.weight.copy_(rnd(512) * 0.1 + 1)
+            ln.bias.copy_(rnd(512) * 0.1)
+        hx = rnd(1, 300, 512)
+        ref = torch.nn.functional.gelu(ln(hx).float()).to(dt)
+        tol_ln = 2e-2 if dtype == "float16" else 1e-4
+        assert float((mt._Hip.layernorm_gelu(hx, ln).float() - ref.float()).abs().max()) <= tol_ln
+        sim = rnd(1, 130, 211).float() * 5
+        z0, z1 = rnd(1, 130, 1).float(), rnd(1, 211, 1).float()
+        ref = mt.log_double_softmax(sim, z0, z1)
+        got = mt._Hip.log_double_softmax(sim, z0, z1)
+        torch.cuda.synchronize()
+        assert float((ref - got).abs().max()) <= 1e-4
