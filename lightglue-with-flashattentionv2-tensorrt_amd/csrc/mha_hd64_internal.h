@@ -76,5 +76,7 @@ int32_t report_error(int32_t status, const char* where, const char* what);
 
 // Diagnostic builds (-DMHA_STAMPS): where the kernel writes its per-workgroup timestamps.
 void set_stamp_buffer(void* p);
+// In-launch split combine on/off (default on unless env MHA_HD64_FUSED_COMBINE=0).
+void set_fused_combine(int enable);
 
 }  // namespace mha_hd64

@@ -37,7 +37,12 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "mha_hd64_internal.h"
 
@@ -60,6 +65,7 @@ constexpr int kTileBytes = kTileKV * kHeadDim * 2;   // 8 KiB fp16 tile
 // One call of a launch (a launch carries up to kMaxCalls independent calls of any shapes: the
 // grouped launcher runs self0+self1 or cross0->1+cross1->0 of a LightGlue layer as one launch).
 constexpr int kMaxCalls = kGroupCalls;
+constexpr int kMaxSplits = 16;  // KV splits per query group (combine loads them all in one round)
 struct CallArgs {
     const void* q;
     const void* k;
@@ -81,6 +87,9 @@ struct FwdArgs {
     int n_calls;
     int total_blocks;            // grid size (kept here so the first scalar-load round has it)
     unsigned long long* stamps;  // diagnostic builds only (MHA_STAMPS): 8 x u64 per workgroup
+    // In-launch combine (non-null): one arrival ticket per query group, indexed by the group's
+    // first block j; zero between launches (the last arriver resets its ticket).
+    unsigned* tickets;
 };
 
 // Uniform (scalar) selection of call ci's arguments from the kernarg table (grouped launches).
@@ -265,6 +274,43 @@ __device__ __forceinline__ void bload8(Raw8<float>& r, __amdgpu_buffer_rsrc_t rs
     r.a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
     r.b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16, soff, 0));
 }
+// cache-policy bits of the buffer intrinsics' aux operand: sc1 (write-through store / L1-bypassing
+// load; the inter-workgroup hand-off form of MI355X_MICROARCH.md)
+constexpr int kSC1 = 16;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+template <int AUX>
+__device__ __forceinline__ void bload8_aux(Raw8<f16>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff) {
+    r.x = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, AUX));
+}
+template <int AUX>
+__device__ __forceinline__ void bload8_aux(Raw8<float>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff) {
+    r.a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, AUX));
+    r.b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16, 0, AUX));
+}
+// One split's term of the split merge, O += w_s·Ô_s, L += w_s with w_s = l_s·2^(m_s - M):
+// shared by the combine kernel and the in-launch combine with contraction off, so both forms
+// round identically (bitwise-equal outputs whichever runs).
+__device__ __forceinline__ float split_weight(float2 ml, float M) {
+#pragma clang fp contract(off)
+    return (ml.x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml.x - M) * ml.y;
+}
+__device__ __forceinline__ void split_accumulate(f32x4& acc, float w, f32x4 v) {
+#pragma clang fp contract(off)
+    acc = acc + w * v;
+}
+// (an fp32 product, then the output rounding: never fused into one mixed-precision FMA)
+__device__ __forceinline__ f32x4 split_scale(f32x4 acc, float inv) {
+#pragma clang fp contract(off)
+    return acc * inv;
+}
+__device__ __forceinline__ void raw8_to_f32(const Raw8<f16>& r, f32x4& lo, f32x4& hi) {
+    lo = f32x4{(float)r.x[0], (float)r.x[1], (float)r.x[2], (float)r.x[3]};
+    hi = f32x4{(float)r.x[4], (float)r.x[5], (float)r.x[6], (float)r.x[7]};
+}
+__device__ __forceinline__ void raw8_to_f32(const Raw8<float>& r, f32x4& lo, f32x4& hi) {
+    lo = r.a;
+    hi = r.b;
+}
 
 // ----------------------------------------------------------------------------------------
 // Main kernel. Grid: x = query blocks of 32*QW rows, y = batch*heads, z = KV splits.
@@ -295,12 +341,17 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     // barrier per step with the LDS work spread over the step.
     constexpr bool PINGPONG = (NT == 512) && (MHA_PINGPONG != 0);
     // Offset halves read one segment apart, so the ping-pong ring needs a fourth stage.
-    constexpr int NSTAGE = PINGPONG ? 4 : 3;
+    // KW = 4 workgroups are the single-super-tile shape: every split is one super-tile (the
+    // planner guarantees it), so one stage suffices.
+    constexpr int NSTAGE = KW == 4 ? 1 : (PINGPONG ? 4 : 3);
     constexpr int NLOAD = (2 * KW * 512) / NT;      // 16-B chunks staged per thread per iteration
     constexpr unsigned SZ = sizeof(TIn);
     static_assert(NLOAD * NT == 2 * KW * 512, "staging must divide evenly");
-    static_assert(NSTAGE * STAGE_BYTES <= 160 * 1024, "LDS ring exceeds 160 KiB");
-    __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE_BYTES];
+    constexpr int OROW = 68;  // epilogue: fp32 row pitch in LDS (64 dims + 4 pad: rows r, r+1 on different banks)
+    constexpr int EPI_BYTES = (KW * BLOCK_M * OROW + KW * BLOCK_M * 2) * 4 + 16;  // + the last-arriver word
+    constexpr int LDS_BYTES = NSTAGE * STAGE_BYTES > EPI_BYTES ? NSTAGE * STAGE_BYTES : EPI_BYTES;
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS exceeds 160 KiB");
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     lds_char* const lds = (lds_char*)smem;
 
     STAMP(0);
@@ -401,10 +452,16 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
 
     // Prologue: stage 0 is published first so QKᵀ(0) starts while the next stage(s) are in flight
     // (published right after it).
+    // (single-stage ring, KW = 4: every split is one super-tile, so the body is straight-line and
+    // the second staging set never exists)
     if (n_iter > 0) issue(0, stgA);
-    if (n_iter > 1) issue(1, stgB);
+    if constexpr (NSTAGE > 1) {
+        if (n_iter > 1) issue(1, stgB);
+    }
     if (n_iter > 0) write(0, stgA);
-    if (n_iter > 2) issue(2, stgA);
+    if constexpr (NSTAGE > 1) {
+        if (n_iter > 2) issue(2, stgA);
+    }
     __syncthreads();
     STAMP(1);
 
@@ -694,6 +751,9 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) mxA[rb] = xhalf_max(tree_max(sA0[rb], sA1[rb]));
     }
+    if constexpr (NSTAGE == 1) {
+        if (n_iter > 0) step(0, sA0, sA1, mxA, sB0, sB1, mxB, F_{}, false, stgA, stgA, false, false);
+    } else {
     if (n_iter > 1) write(1, stgB);
     if constexpr (NSTAGE == 4) {
         if (n_iter > 3) issue(3, stgB);
@@ -735,6 +795,7 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     }
     if (it < n_iter) step(it, sA0, sA1, mxA, sB0, sB1, mxB, F_{}, false, stg0, stg1, false, false);
     if (PINGPONG && !late_half) __syncthreads();
+    }  // NSTAGE > 1
     STAMP(2);
 
     // ---- epilogue ----
@@ -743,10 +804,8 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     // chunks (a wave stores complete rows: coalesced, few store instructions).
     // A wave that saw no key (all of its tiles past nkv) gets m = -inf (weight 0). The test uses
     // the cross-half total: the halves hold disjoint keys but the SAME query's m and O dims.
-    constexpr int OROW = 68;  // fp32 row pitch in LDS: 64 dims + 4 pad (rows r, r+1 on different banks)
     float* ol = reinterpret_cast<float*>(smem);     // [KW][BLOCK_M][OROW]
     float* mlb = ol + KW * BLOCK_M * OROW;          // [KW][BLOCK_M][2]
-    static_assert((KW * BLOCK_M * OROW + KW * BLOCK_M * 2) * 4 <= NSTAGE * STAGE_BYTES, "epilogue LDS");
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
         const float L_w = l_acc[rb][0];  // the row-sum MFMA already spans both half-waves
@@ -774,21 +833,26 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     const __amdgpu_buffer_rsrc_t po_rs =
         make_rsrc(reinterpret_cast<TOut*>(ca.part_o) + (size_t)bh * ca.splits * nq * kHeadDim,
                   (unsigned)(ca.splits * nq * kHeadDim * sizeof(TOut)));
-#pragma unroll
-    for (int pass = 0; pass < (BLOCK_M * 8) / NT; ++pass) {
-        const int idx = pass * NT + tid;
-        const int row = idx >> 3;
-        const int c8 = (idx & 7) * 8;
-        const int q = q_base + row;
-        float M = -INFINITY;
+    // In-launch combine: every split's workgroup publishes its partial write-through (sc1) and
+    // takes a ticket; the group's last arriver reads all the group's partials back and writes O
+    // (same arithmetic and order as the combine kernel, so both forms give the same bits). Visibility follows MI355X_MICROARCH.md "Valid forms" (table
+    // row 1): all partial bytes stored sc1 and drained (vmcnt(0)) before one lane's agent-scope
+    // add, every load of them an sc1 buffer load, the other waves behind a barrier.
+    const bool fused = a.tickets != nullptr && ca.splits > 1;
+    const __amdgpu_buffer_rsrc_t pml_rs =
+        make_rsrc(ca.part_ml + (size_t)bh * ca.splits * nq, (unsigned)(ca.splits * nq * sizeof(float2)));
+    // merge of the KW key-wave partials of (row, dims c8..c8+7) staged in LDS
+    auto merge_waves = [&](int row, int c8, float& M, float& L, f32x4& acc0, f32x4& acc1) {
+        M = -INFINITY;
         float2 ml[KW];
 #pragma unroll
         for (int k = 0; k < KW; ++k) {
             ml[k] = *reinterpret_cast<const float2*>(mlb + (k * BLOCK_M + row) * 2);
             M = fmaxf(M, ml[k].x);
         }
-        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        float L = 0.f;
+        acc0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+        L = 0.f;
 #pragma unroll
         for (int k = 0; k < KW; ++k) {
             const float w = (ml[k].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[k].x - M);
@@ -797,6 +861,16 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
             acc0 += w * *reinterpret_cast<const f32x4*>(src);
             acc1 += w * *reinterpret_cast<const f32x4*>(src + 4);
         }
+    };
+#pragma unroll
+    for (int pass = 0; pass < (BLOCK_M * 8) / NT; ++pass) {
+        const int idx = pass * NT + tid;
+        const int row = idx >> 3;
+        const int c8 = (idx & 7) * 8;
+        const int q = q_base + row;
+        float M, L;
+        f32x4 acc0, acc1;
+        merge_waves(row, c8, M, L, acc0, acc1);
         if (q < nq && !(MHA_ABL & ABL_NO_STORE)) {
             if (ca.splits == 1) {
                 const float inv = 1.f / L;
@@ -806,9 +880,74 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
                 // the fp16 path; the fp32-output path keeps fp32), merged with weights l_s·2^(m_s-M).
                 const unsigned prow = (unsigned)(split * nq + q);
                 const float inv = (L > 0.f) ? 1.f / L : 0.f;
-                store8<TOut, MHA_PART_AUX>(po_rs, prow * (unsigned)(kHeadDim * sizeof(TOut)) + c8 * (unsigned)sizeof(TOut),
-                                           acc0 * inv, acc1 * inv);
-                if (c8 == 0) ca.part_ml[((size_t)bh * ca.splits) * nq + prow] = make_float2(M, L);
+                const unsigned poff = prow * (unsigned)(kHeadDim * sizeof(TOut)) + c8 * (unsigned)sizeof(TOut);
+                if (fused) {
+                    store8<TOut, kSC1>(po_rs, poff, acc0 * inv, acc1 * inv);
+                    if (c8 == 0)
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(M, L)), pml_rs,
+                                                              prow * (unsigned)sizeof(float2), 0, kSC1);
+                } else {
+                    store8<TOut, MHA_PART_AUX>(po_rs, poff, acc0 * inv, acc1 * inv);
+                    if (c8 == 0) ca.part_ml[((size_t)bh * ca.splits) * nq + prow] = make_float2(M, L);
+                }
+            }
+        }
+    }
+    if (fused) {  // workgroup-uniform
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        unsigned* last_word = reinterpret_cast<unsigned*>(smem + EPI_BYTES - 16);
+        if (tid == 0) {
+            unsigned* t = a.tickets + (j - split);
+            const unsigned old = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned last = old + 1 == (unsigned)ca.splits;
+            if (last) __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *last_word = last;
+        }
+        __syncthreads();
+        if (*last_word) {
+#pragma unroll
+            for (int pass = 0; pass < (BLOCK_M * 8) / NT; ++pass) {
+                const int idx = pass * NT + tid;
+                const int row = idx >> 3;
+                const int c8 = (idx & 7) * 8;
+                const int q = q_base + row;
+                if (q >= nq) continue;
+                // every split's partial as stored (its own too), merged in split order exactly as
+                // the combine kernel does: the result does not depend on which split came last
+                float2 ml[kMaxSplits];
+                Raw8<TOut> pv[kMaxSplits];
+#pragma unroll
+                for (int s2 = 0; s2 < kMaxSplits; ++s2) {
+                    if (s2 < ca.splits) {
+                        const unsigned prow = (unsigned)(s2 * nq + q);
+                        ml[s2] = __builtin_bit_cast(
+                            float2, __builtin_amdgcn_raw_buffer_load_b64(pml_rs, prow * (unsigned)sizeof(float2), 0, kSC1));
+                        bload8_aux<kSC1>(pv[s2], po_rs,
+                                         prow * (unsigned)(kHeadDim * sizeof(TOut)) + c8 * (unsigned)sizeof(TOut));
+                    }
+                }
+                float Mt = -INFINITY;
+#pragma unroll
+                for (int s2 = 0; s2 < kMaxSplits; ++s2)
+                    if (s2 < ca.splits) Mt = fmaxf(Mt, ml[s2].x);
+                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+                float L = 0.f;
+#pragma unroll
+                for (int s2 = 0; s2 < kMaxSplits; ++s2) {
+                    if (s2 < ca.splits) {
+                        const float w = split_weight(ml[s2], Mt);
+                        L += w;
+                        f32x4 lo, hi;
+                        raw8_to_f32(pv[s2], lo, hi);
+                        split_accumulate(acc0, w, lo);
+                        split_accumulate(acc1, w, hi);
+                    }
+                }
+                const float inv = 1.f / L;
+                if (!(MHA_ABL & ABL_NO_STORE))
+                    store8<TOut, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c8) * sizeof(TOut)),
+                                             split_scale(acc0, inv), split_scale(acc1, inv));
             }
         }
     }
@@ -829,7 +968,6 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
 // Block b serves XCD b % 8: it combines rows whose partials the main kernel produced on that same XCD (same bijective block order), so the reads hit L2. All
 // partials of a row are loaded in one round trip (S <= kMaxSplits).
 // ----------------------------------------------------------------------------------------
-constexpr int kMaxSplits = 16;
 
 struct CombineCall {
     const void* part_o;
@@ -923,14 +1061,14 @@ __global__ __launch_bounds__(256) void mha_hd64_combine_kernel(CombineArgs c) {
 #pragma unroll
     for (int s = 0; s < kMaxSplits; ++s) {
         if (s < cc.splits) {
-            const float w = (ml[s].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[s].x - M) * ml[s].y;
+            const float w = split_weight(ml[s], M);
             L += w;
-            acc += w * v[s];
+            split_accumulate(acc, w, v[s]);
         }
     }
-    const float inv = 1.f / L;
+    const f32x4 o = split_scale(acc, 1.f / L);
     TOut* out = reinterpret_cast<TOut*>(cc.out) + ((size_t)bh * cc.nq + q) * kHeadDim + chunk * 4;
-    store4<TOut>(out, acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+    store4<TOut>(out, o[0], o[1], o[2], o[3]);
 }
 
 template <typename TIn, typename TOut, int QW, int KW, int RB, bool MULTI>
@@ -956,6 +1094,7 @@ hipError_t launch_fwd_shape(const FwdArgs& a, int grid, int qw, int kw, int rb, 
         case 64 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 1, false>(a, grid, stream);
         case 64 + 1 * 8 + 2: return launch_fwd<TIn, TOut, 1, 2, 1, false>(a, grid, stream);
         case 64 + 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2, 1, false>(a, grid, stream);
+        case 64 + 2 * 8 + 4: return launch_fwd<TIn, TOut, 2, 4, 1, false>(a, grid, stream);
         case 128 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 2, false>(a, grid, stream);
         default: return hipErrorInvalidValue;
     }
@@ -972,7 +1111,8 @@ hipError_t launch_combine(const CombineArgs& c, hipStream_t stream) {
 
 bool valid_shape(int qw, int kw, int rb) {
     if (rb == 2) return qw == 2 && kw == 2;
-    return rb == 1 && ((qw == 4 && kw == 1) || (qw == 2 && kw == 2) || (qw == 1 && kw == 2) || (qw == 4 && kw == 2));
+    return rb == 1 && ((qw == 4 && kw == 1) || (qw == 2 && kw == 2) || (qw == 1 && kw == 2) || (qw == 4 && kw == 2) ||
+                       (qw == 2 && kw == 4));
 }
 
 unsigned long long* g_stamps = nullptr;  // diagnostic builds (MHA_STAMPS) only
@@ -982,6 +1122,53 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 }  // namespace
 
 void set_stamp_buffer(void* p) { g_stamps = reinterpret_cast<unsigned long long*>(p); }
+
+// ---- arrival tickets of the in-launch combine ----
+// One zeroed device array per (device, stream): launches on one stream are serialised, and each
+// launch leaves every ticket it used at zero (the last arriver resets it), so the array needs no
+// per-call reset. Arrays are created (hipMalloc + a memset ordered on the stream) only outside
+// stream capture; a launch that finds none (first use under capture) combines in a second kernel.
+// Grown arrays are kept alive (a launch in flight may still use the old one).
+namespace {
+int g_fused = -1;  // -1: unset (env MHA_HD64_FUSED_COMBINE, default on), 0 off, 1 on
+std::mutex g_ticket_mu;
+std::map<std::pair<int, hipStream_t>, std::pair<unsigned*, int>> g_tickets;
+std::vector<unsigned*> g_retired;
+}  // namespace
+
+void set_fused_combine(int enable) {
+    std::lock_guard<std::mutex> lk(g_ticket_mu);
+    g_fused = enable ? 1 : 0;
+}
+
+static bool fused_enabled() {
+    std::lock_guard<std::mutex> lk(g_ticket_mu);
+    if (g_fused < 0) {
+        const char* e = std::getenv("MHA_HD64_FUSED_COMBINE");
+        g_fused = (e && e[0] == '0') ? 0 : 1;
+    }
+    return g_fused == 1;
+}
+
+static unsigned* tickets_for(hipStream_t stream, int count) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_ticket_mu);
+    auto& slot = g_tickets[{dev, stream}];
+    if (slot.first && slot.second >= count) return slot.first;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    const int cap = std::max(count, 4096);
+    unsigned* p = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&p), (size_t)cap * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, (size_t)cap * sizeof(unsigned), stream) != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+    }
+    if (slot.first) g_retired.push_back(slot.first);
+    slot = {p, cap};
+    return p;
+}
 
 size_t split_workspace_bytes(const Call& c, int splits) {
     if (splits <= 1) return 0;
@@ -1006,6 +1193,15 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
         } else {
             qw = 2;
             kw = 2;
+            // A single call that needs a KV split: one 256-key super-tile per split (the (2,4)
+            // shape: the shortest per-workgroup chain) while that grid stays within one residency
+            // round (2 workgroups per CU by LDS).
+            if (n == 1) {
+                const Call& c = calls[0];
+                const long g64 = (long)c.batch * c.heads * ((c.nq + 63) / 64);
+                const long st = (c.nkv + 255) / 256;
+                if (g64 < 256 && st <= kMaxSplits && g64 * st <= 512) kw = 4;
+            }
         }
     }
     p.q_waves = qw;
@@ -1017,6 +1213,23 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
         groups += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + block_m - 1) / block_m);
     int want = force_splits > 0 ? force_splits : (int)std::max(1L, (256 + groups - 1) / std::max(1L, groups));
     want = std::max(1, std::min(want, kMaxSplits));
+    if (kw == 4) {
+        // single-super-tile shape: every split must be exactly one super-tile (its LDS ring has
+        // one stage); otherwise (too many keys, or no workspace for the partials) use (2,2).
+        size_t off = 0;
+        bool ok = true;
+        for (int i = 0; i < n; ++i) {
+            const int super_total = std::max(1, (calls[i].nkv + 255) / 256);
+            ok = ok && super_total <= kMaxSplits;
+            p.splits[i] = super_total;
+            p.tiles_per_split[i] = 1;
+            p.ws_offset[i] = off;
+            off += split_workspace_bytes(calls[i], super_total);
+        }
+        p.ws_needed = off;
+        if (ok && off <= ws_bytes) return p;
+        return plan_group(calls, n, ws_bytes, 2, 2, force_splits);
+    }
     for (;;) {
         size_t off = 0;
         for (int i = 0; i < n; ++i) {
@@ -1091,6 +1304,9 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
     a.n_calls = n_live;
     a.total_blocks = blocks;
     const int rbw = p.rows_per_wave / 32;
+    // Split calls combine inside the main launch when a ticket array is available (phase_mask 3,
+    // the production form); otherwise (or MHA_HD64_FUSED_COMBINE=0) in the combine kernel.
+    if (any_split && (phase_mask & 3) == 3 && fused_enabled()) a.tickets = tickets_for(stream, blocks);
     hipError_t e = hipSuccess;
     if (phase_mask & 1) {
         if (in == InType::F16) {
@@ -1101,7 +1317,7 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
                                       : launch_fwd_shape<float, float>(a, blocks, p.q_waves, p.kv_waves, rbw, stream);
         }
     }
-    if (e != hipSuccess || !any_split || !(phase_mask & 2)) return e;
+    if (e != hipSuccess || !any_split || !(phase_mask & 2) || a.tickets) return e;
     // Combine grid: for every XCD x, the groups (of calls that split) whose first split block
     // ran on x (same bijective order as the main kernel), 16 rows per block.
     cb.n_calls = n_live;

@@ -355,7 +355,7 @@ const char* mha_hd64_last_error(void) { return g_last_error.c_str(); }
 void mha_hd64_set_abort_on_error(int32_t enable) { g_abort_on_error = enable != 0; }
 const char* mha_hd64_build_info(void) {
     return "mha_hd64: gfx950 (CDNA4) HIP kernels, v_mfma_f32_32x32x16_f16 + ds_read_b64_tr_b16; "
-           "variants fp16->fp16, fp16->fp32, fp32->fp32; workgroups (q,kv waves) 4x1 2x2 1x2 4x2; software-pipelined QK(t+1)|softmax(t); split-KV combine";
+           "variants fp16->fp16, fp16->fp32, fp32->fp32; workgroups (q,kv waves) 4x1 2x2 1x2 4x2 2x4, 2x2 with 64-row waves; software-pipelined QK(t+1)|softmax(t); split-KV combine";
 }
 
 // Test/bench hook (not part of include/mha_hd64.h): launch with a forced plan
@@ -370,9 +370,12 @@ int32_t mha_hd64_launch_forced(const void* q, const void* k, const void* v, void
     const mha_hd64::Call c{q, k, v, o, batch, heads, nq, nkv};
     const mha_hd64::LaunchPlan plan = mha_hd64::plan_call(c, workspace ? ws_bytes : 0, q_waves, kv_waves, splits);
     const int plan_qw = plan.q_waves + (plan.rows_per_wave == 64 ? 10 : 0);
-    if (q_waves != 0 && (plan_qw != q_waves || plan.kv_waves != kv_waves))
+    // (2,4) takes one split per 256-key super-tile and falls back to (2,2) past 16 of them
+    const bool single_tile = q_waves == 2 && kv_waves == 4;
+    const bool fell_back = single_tile && plan_qw == 2 && plan.kv_waves == 2;
+    if (q_waves != 0 && !fell_back && (plan_qw != q_waves || plan.kv_waves != kv_waves))
         return fail(MHA_HD64_STATUS_BAD_PARAM, __FILE__, __LINE__, "forced workgroup shape is not compiled");
-    if (splits > 1 && plan.splits != splits)
+    if (splits > 1 && !single_tile && plan.splits != splits)
         return fail(MHA_HD64_STATUS_WORKSPACE, __FILE__, __LINE__, "forced split does not fit the workspace/keys");
     return launch_status(mha_hd64::launch_attention(c, in_f32 ? mha_hd64::InType::F32 : mha_hd64::InType::F16,
                                                     out_f32 ? mha_hd64::OutType::F32 : mha_hd64::OutType::F16,
@@ -383,6 +386,9 @@ int32_t mha_hd64_launch_forced(const void* q, const void* k, const void* v, void
 
 // Diagnostic hook: per-workgroup timestamp buffer for -DMHA_STAMPS builds (ignored otherwise).
 void mha_hd64_set_stamp_buffer(void* p) { mha_hd64::set_stamp_buffer(p); }
+
+// Test/bench hook: 1 = split calls combine inside the main launch (default), 0 = combine kernel.
+void mha_hd64_set_fused_combine(int32_t enable) { mha_hd64::set_fused_combine(enable); }
 
 // Plan query hook for tests/bench: fills {q_waves, kv_waves, splits, tiles_per_split}; returns workspace bytes.
 size_t mha_hd64_plan(int32_t batch, int32_t heads, int32_t nq, int32_t nkv, size_t ws_bytes, int32_t* out4) {

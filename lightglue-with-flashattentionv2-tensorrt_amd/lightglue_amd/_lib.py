@@ -134,6 +134,7 @@ HOOKS = {
     "mha_hd64_launch_forced": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _S, _P, _I], _I),
     "mha_hd64_plan": ([_I, _I, _I, _I, _S, ctypes.POINTER(ctypes.c_int32)], _S),
     "mha_hd64_set_stamp_buffer": ([_P], None),
+    "mha_hd64_set_fused_combine": ([_I], None),
 }
 
 _lib = None

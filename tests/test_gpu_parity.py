@@ -78,8 +78,10 @@ def test_fp16in_fp32out_launcher(name, dev):
 
 
 # ---- every launch plan (query-wave split x cross-workgroup KV split) against the C oracle ----
-PLAN_SHAPES = [(1, 1), (33, 65), (100, 100), (64, 2048), (300, 129), (1024, 1024), (257, 1000)]
-WG_SHAPES = [(4, 1), (2, 2), (1, 2), (4, 2), (12, 2)]  # 12 = two 32-row query blocks per wave, 2 q-waves
+PLAN_SHAPES = [(1, 1), (33, 65), (100, 100), (64, 2048), (300, 129), (1024, 1024), (257, 1000), (16, 4500)]
+# 12 = two 32-row query blocks per wave, 2 q-waves; (2, 4) = one 256-key super-tile per split
+# (the split count follows from nkv; past 16 super-tiles the planner falls back to (2, 2))
+WG_SHAPES = [(4, 1), (2, 2), (1, 2), (4, 2), (12, 2), (2, 4)]
 
 
 @pytest.mark.parametrize("nq,nkv", PLAN_SHAPES)
@@ -90,6 +92,8 @@ def test_forced_plans_match_oracle(nq, nkv, wg, splits, dev, oracle_mod):
 
     q_waves, kv_waves = wg
     super_total = -(-nkv // (64 * kv_waves))
+    if kv_waves == 4 and splits != 1:
+        pytest.skip("(2, 4) takes one split per super-tile")
     if splits > super_total:
         pytest.skip("more splits than key tiles")
     if -(-super_total // -(-super_total // splits)) != splits:
@@ -333,3 +337,87 @@ def test_grouped_matches_single_calls_bitwise_when_plans_agree(dev):
     (b,) = mha_hd64_grouped([(q, k, v)])
     torch.cuda.synchronize()
     assert torch.equal(a, b)
+
+
+# ---- in-launch split combine (arrival tickets; csrc/mha_hd64_kernels.hip epilogue) ----
+FUSED_SHAPES = [  # (nq, nkv, q_waves, kv_waves, splits)
+    (1024, 1024, 2, 4, 0), (1024, 1024, 2, 2, 4), (300, 2048, 2, 2, 3), (100, 1000, 12, 2, 3),
+    (64, 4000, 2, 4, 0), (33, 65, 4, 1, 2), (257, 1000, 4, 2, 2)]
+
+
+def _forced(lib, q, k, v, o, nq, nkv, qw, kw, sp, ws, stream=None):
+    from lightglue_amd import _lib
+
+    st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), 1, 4, nq, nkv,
+                                    int(q.dtype == torch.float32), int(o.dtype == torch.float32), qw, kw, sp,
+                                    ws.data_ptr(), ws.numel(),
+                                    (stream or torch.cuda.current_stream()).cuda_stream, 3)
+    assert st == 0, _lib.last_error()
+
+
+@pytest.fixture
+def fused_switch(dev):
+    from lightglue_amd import _lib
+
+    lib = _lib.load()
+    yield lib.mha_hd64_set_fused_combine
+    lib.mha_hd64_set_fused_combine(1)
+
+
+@pytest.mark.parametrize("out_dt", [torch.float16, torch.float32])
+def test_fused_combine_bitwise_equals_combine_kernel(out_dt, dev, fused_switch, oracle_mod):
+    """The last-arriver combine reads every split back in split order: same bits as the kernel."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+    for nq, nkv, qw, kw, sp in FUSED_SHAPES:
+        qn, kn, vn = synth.qkv(77 + nq + nkv, nq, nkv)
+        q, k, v = (_t(x, dev, torch.float16) for x in (qn, kn, vn))
+        outs = []
+        for fused in (0, 1):
+            fused_switch(fused)
+            o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
+            _forced(lib, q, k, v, o, nq, nkv, qw, kw, sp, ws)
+            outs.append(o)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), (nq, nkv, qw, kw, sp)
+        rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 32)), nq - 1])
+        ref = oracle_mod.attention_c(np.ascontiguousarray(synth.round_f16(qn)[:, :, rows]), synth.round_f16(kn),
+                                     synth.round_f16(vn))
+        assert _maxdiff(outs[1].float().cpu().numpy()[:, :, rows], ref) <= TOL
+
+
+def test_fused_combine_tickets_reset_under_load(dev, fused_switch):
+    """Many launches with different split counts on one stream reuse the same tickets (each
+    launch leaves them at zero), while another stream keeps the chip busy (uneven load)."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+    cases = []
+    for nq, nkv, qw, kw, sp in FUSED_SHAPES:
+        qn, kn, vn = synth.qkv(5 + nq + 3 * nkv, nq, nkv)
+        q, k, v = (_t(x, dev, torch.float16) for x in (qn, kn, vn))
+        fused_switch(0)
+        o = torch.empty_like(q)
+        _forced(lib, q, k, v, o, nq, nkv, qw, kw, sp, ws)
+        cases.append((q, k, v, o, nq, nkv, qw, kw, sp))
+    torch.cuda.synchronize()
+    fused_switch(1)
+    s = torch.cuda.Stream()
+    busy = torch.cuda.Stream()
+    a = torch.randn(4096, 4096, device=dev, dtype=torch.float16)
+    outs = []
+    with torch.cuda.stream(busy):
+        for _ in range(6):
+            a = (a @ a).clamp_(-1, 1)
+    with torch.cuda.stream(s):
+        for r in range(8):
+            for i, (q, k, v, _, nq, nkv, qw, kw, sp) in enumerate(cases):
+                o = torch.full_like(q, float("nan"))
+                _forced(lib, q, k, v, o, nq, nkv, qw, kw, sp, ws, stream=s)
+                outs.append((i, o))
+    torch.cuda.synchronize()
+    for i, o in outs:
+        assert torch.equal(o, cases[i][3]), i

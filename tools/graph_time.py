@@ -84,13 +84,21 @@ def main():
     for lname, lib in libs:
         for name, b, nq, nkv, qw, kw, sp in shapes:
             q, k, v, o = data[name]
-            for mask, tag in (((1, "main"), (3, "all"), (2, "comb")) if os.environ.get("GT_ALL") else ((1, "main"),)):
+            tags = ((1, "main"), (3, "all"), (2, "comb"), (3, "all2k")) if os.environ.get("GT_ALL") else ((1, "main"),)
+            for mask, tag in tags:
+                # "all": the production form (split calls combine inside the main launch when the
+                # library has that path); "all2k": main kernel + combine kernel
+                fused = hasattr(lib, "mha_hd64_set_fused_combine")
+                if fused:
+                    lib.mha_hd64_set_fused_combine(0 if tag == "all2k" else 1)
                 def fn(lib=lib, q=q, k=k, v=v, o=o, b=b, nq=nq, nkv=nkv, mask=mask, qw=qw, kw=kw, sp=sp):
                     st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), b, 4,
                                                     nq, nkv, 0, 0, qw, kw, sp, ws.data_ptr(), ws.numel(),
                                                     torch.cuda.current_stream().cuda_stream, mask)
                     assert st == 0
                 cases.append((f"{lname}:{name}:{tag}", graph_of(fn, stream)))
+                if fused:
+                    lib.mha_hd64_set_fused_combine(1)
     x = torch.zeros(1, device=dev)
     cases.append(("torch_add1", graph_of(lambda: x.add_(1), stream)))
     res = {c: [] for c, _ in cases}
