@@ -78,5 +78,7 @@ int32_t report_error(int32_t status, const char* where, const char* what);
 void set_stamp_buffer(void* p);
 // In-launch split combine on/off (default on unless env MHA_HD64_FUSED_COMBINE=0).
 void set_fused_combine(int enable);
+// How the calling thread's last launch merged its splits: 0 none, 1 in-launch, 2 combine kernel.
+int last_combine_form();
 
 }  // namespace mha_hd64

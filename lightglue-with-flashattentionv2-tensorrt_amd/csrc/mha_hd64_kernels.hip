@@ -1124,17 +1124,31 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 void set_stamp_buffer(void* p) { g_stamps = reinterpret_cast<unsigned long long*>(p); }
 
 // ---- arrival tickets of the in-launch combine ----
-// One zeroed device array per (device, stream): launches on one stream are serialised, and each
-// launch leaves every ticket it used at zero (the last arriver resets it), so the array needs no
-// per-call reset. Arrays are created (hipMalloc + a memset ordered on the stream) only outside
-// stream capture; a launch that finds none (first use under capture) combines in a second kernel.
-// Grown arrays are kept alive (a launch in flight may still use the old one).
+// Every ticket a launch uses is zero when it starts and zero when it ends (the last arriver of
+// each group resets its own), so a ticket array needs no per-call reset as long as no two launches
+// that use it run concurrently:
+//  * eager launches: one array per (device, stream) -- launches on one stream are serialised;
+//  * launches recorded under stream capture: a slice of their own, carved from a per-device arena
+//    (an instantiated graph never runs concurrently with itself, while two graphs captured on one
+//    stream may be replayed side by side).
+// Arrays are created only outside capture (hipMalloc + memset, then a one-time stream sync for the
+// arena); a launch that finds no tickets combines in the second kernel instead. Nothing is freed
+// (a launch in flight or a graph may still reference it).
 namespace {
 int g_fused = -1;  // -1: unset (env MHA_HD64_FUSED_COMBINE, default on), 0 off, 1 on
 std::mutex g_ticket_mu;
 std::map<std::pair<int, hipStream_t>, std::pair<unsigned*, int>> g_tickets;
-std::vector<unsigned*> g_retired;
+struct Arena {
+    unsigned* base = nullptr;
+    int cap = 0;
+    int used = 0;
+};
+std::map<int, Arena> g_arena;
+thread_local int g_last_combine = 0;  // this thread's last launch: 0 no split, 1 in-launch, 2 kernel
+constexpr int kArenaTickets = 1 << 20;  // 4 MiB per device
 }  // namespace
+
+int last_combine_form() { return g_last_combine; }
 
 void set_fused_combine(int enable) {
     std::lock_guard<std::mutex> lk(g_ticket_mu);
@@ -1150,22 +1164,40 @@ static bool fused_enabled() {
     return g_fused == 1;
 }
 
-static unsigned* tickets_for(hipStream_t stream, int count) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(g_ticket_mu);
-    auto& slot = g_tickets[{dev, stream}];
-    if (slot.first && slot.second >= count) return slot.first;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    const int cap = std::max(count, 4096);
+static unsigned* zeroed_tickets(int count, hipStream_t stream) {
     unsigned* p = nullptr;
-    if (hipMalloc(reinterpret_cast<void**>(&p), (size_t)cap * sizeof(unsigned)) != hipSuccess) return nullptr;
-    if (hipMemsetAsync(p, 0, (size_t)cap * sizeof(unsigned), stream) != hipSuccess) {
+    if (hipMalloc(reinterpret_cast<void**>(&p), (size_t)count * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, (size_t)count * sizeof(unsigned), stream) != hipSuccess) {
         (void)hipFree(p);
         return nullptr;
     }
-    if (slot.first) g_retired.push_back(slot.first);
+    return p;
+}
+
+static unsigned* tickets_for(hipStream_t stream, int count) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_ticket_mu);
+    Arena& ar = g_arena[dev];
+    if (cs != hipStreamCaptureStatusNone) {  // a slice owned by this recorded launch
+        const int n = (count + 63) & ~63;
+        if (!ar.base || ar.used + n > ar.cap) return nullptr;
+        unsigned* p = ar.base + ar.used;
+        ar.used += n;
+        return p;
+    }
+    if (!ar.base) {  // first eager launch on this device: the arena for later captures
+        ar.base = zeroed_tickets(kArenaTickets, stream);
+        if (ar.base && hipStreamSynchronize(stream) == hipSuccess) ar.cap = kArenaTickets;
+        else ar.base = nullptr;
+    }
+    auto& slot = g_tickets[{dev, stream}];
+    if (slot.first && slot.second >= count) return slot.first;
+    const int cap = std::max(count, 4096);
+    unsigned* p = zeroed_tickets(cap, stream);
+    if (!p) return nullptr;
     slot = {p, cap};
     return p;
 }
@@ -1307,6 +1339,7 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
     // Split calls combine inside the main launch when a ticket array is available (phase_mask 3,
     // the production form); otherwise (or MHA_HD64_FUSED_COMBINE=0) in the combine kernel.
     if (any_split && (phase_mask & 3) == 3 && fused_enabled()) a.tickets = tickets_for(stream, blocks);
+    g_last_combine = !any_split ? 0 : (a.tickets ? 1 : 2);
     hipError_t e = hipSuccess;
     if (phase_mask & 1) {
         if (in == InType::F16) {

@@ -389,6 +389,8 @@ void mha_hd64_set_stamp_buffer(void* p) { mha_hd64::set_stamp_buffer(p); }
 
 // Test/bench hook: 1 = split calls combine inside the main launch (default), 0 = combine kernel.
 void mha_hd64_set_fused_combine(int32_t enable) { mha_hd64::set_fused_combine(enable); }
+// Test hook: 0 = the calling thread's last launch had no split, 1 = in-launch combine, 2 = combine kernel.
+int32_t mha_hd64_last_combine_form(void) { return mha_hd64::last_combine_form(); }
 
 // Plan query hook for tests/bench: fills {q_waves, kv_waves, splits, tiles_per_split}; returns workspace bytes.
 size_t mha_hd64_plan(int32_t batch, int32_t heads, int32_t nq, int32_t nkv, size_t ws_bytes, int32_t* out4) {

@@ -236,6 +236,9 @@ def test_graph_capture_replay(dev):
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
         mha_hd64(q, k, v, out=out)
+    from lightglue_amd import _lib
+
+    assert _lib.load().mha_hd64_last_combine_form() == 1  # one launch, splits merged in it
     out.zero_()
     g.replay()
     torch.cuda.synchronize()
@@ -379,6 +382,7 @@ def test_fused_combine_bitwise_equals_combine_kernel(out_dt, dev, fused_switch, 
             fused_switch(fused)
             o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
             _forced(lib, q, k, v, o, nq, nkv, qw, kw, sp, ws)
+            assert lib.mha_hd64_last_combine_form() == (1 if fused else 2)
             outs.append(o)
         torch.cuda.synchronize()
         assert torch.equal(outs[0], outs[1]), (nq, nkv, qw, kw, sp)
@@ -421,3 +425,38 @@ def test_fused_combine_tickets_reset_under_load(dev, fused_switch):
     torch.cuda.synchronize()
     for i, o in outs:
         assert torch.equal(o, cases[i][3]), i
+
+
+def test_fused_combine_graphs_from_one_stream_replayed_concurrently(dev):
+    """Two graphs captured on one stream own separate tickets: replaying them side by side on two
+    streams (each graph with its own workspace, the reference's rule) gives the eager results."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    cap = torch.cuda.Stream()
+    data = []
+    for seed, (nq, nkv) in ((31, (1024, 1024)), (32, (512, 2048))):
+        qn, kn, vn = synth.qkv(seed, nq, nkv)
+        q, k, v = (_t(x, dev, torch.float16) for x in (qn, kn, vn))
+        ws = torch.empty(16 << 20, dtype=torch.uint8, device=dev)
+        ref = torch.empty_like(q)
+        _forced(lib, q, k, v, ref, nq, nkv, 0, 0, 0, ws)
+        data.append((q, k, v, ref, torch.empty_like(q), ws, nq, nkv))
+    torch.cuda.synchronize()
+    graphs = []
+    for q, k, v, _, out, ws, nq, nkv in data:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cap):
+            _forced(lib, q, k, v, out, nq, nkv, 0, 0, 0, ws, stream=cap)
+        assert lib.mha_hd64_last_combine_form() == 1  # recorded with its own tickets
+        graphs.append(g)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for _ in range(20):
+        for d, g, s in zip(data, graphs, streams):
+            d[4].zero_()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                g.replay()
+        for d, s in zip(data, streams):
+            torch.cuda.current_stream().wait_stream(s)
+            assert torch.equal(d[4], d[3])
