@@ -905,6 +905,7 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
             *last_word = last;
         }
         __syncthreads();
+        STAMP(5);
         if (*last_word) {
 #pragma unroll
             for (int pass = 0; pass < (BLOCK_M * 8) / NT; ++pass) {
@@ -1078,7 +1079,7 @@ hipError_t launch_fwd(const FwdArgs& a, int grid, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// Grouped launches (several calls) exist for the two shapes the planner picks on its own.
+// Grouped launches (several calls) exist for the shapes the planner picks on its own.
 template <typename TIn, typename TOut>
 hipError_t launch_fwd_shape(const FwdArgs& a, int grid, int qw, int kw, int rb, hipStream_t stream) {
     if (a.n_calls > 1) {
@@ -1086,6 +1087,7 @@ hipError_t launch_fwd_shape(const FwdArgs& a, int grid, int qw, int kw, int rb, 
             case 64 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 1, true>(a, grid, stream);
             case 64 + 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2, 1, true>(a, grid, stream);
             case 128 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 2, true>(a, grid, stream);
+            case 64 + 2 * 8 + 4: return launch_fwd<TIn, TOut, 2, 4, 1, true>(a, grid, stream);
             default: return hipErrorInvalidValue;
         }
     }
@@ -1225,15 +1227,19 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
         } else {
             qw = 2;
             kw = 2;
-            // A single call that needs a KV split: one 256-key super-tile per split (the (2,4)
-            // shape: the shortest per-workgroup chain) while that grid stays within one residency
-            // round (2 workgroups per CU by LDS).
-            if (n == 1) {
-                const Call& c = calls[0];
-                const long g64 = (long)c.batch * c.heads * ((c.nq + 63) / 64);
-                const long st = (c.nkv + 255) / 256;
-                if (g64 < 256 && st <= kMaxSplits && g64 * st <= 512) kw = 4;
+            // A launch that needs a KV split: one 256-key super-tile per split (the (2,4) shape:
+            // the shortest per-workgroup chain) while that grid stays within one residency round
+            // (2 workgroups per CU by LDS).
+            long g64 = 0, wgs = 0;
+            bool fits = true;
+            for (int i = 0; i < n; ++i) {
+                const long g = (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 63) / 64);
+                const long st = (calls[i].nkv + 255) / 256;
+                fits = fits && st <= kMaxSplits;
+                g64 += g;
+                wgs += g * st;
             }
+            if (g64 < 256 && fits && wgs <= 512) kw = 4;
         }
     }
     p.q_waves = qw;
