@@ -343,7 +343,7 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     // Offset halves read one segment apart, so the ping-pong ring needs a fourth stage.
     // KW = 4 workgroups are the single-super-tile shape: every split is one super-tile (the
     // planner guarantees it), so one stage suffices.
-    constexpr int NSTAGE = KW == 4 ? 1 : (PINGPONG ? 4 : 3);
+    constexpr int NSTAGE = KW >= 4 ? 1 : (PINGPONG ? 4 : 3);
     constexpr int NLOAD = (2 * KW * 512) / NT;      // 16-B chunks staged per thread per iteration
     constexpr unsigned SZ = sizeof(TIn);
     static_assert(NLOAD * NT == 2 * KW * 512, "staging must divide evenly");
@@ -862,9 +862,15 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
             acc1 += w * *reinterpret_cast<const f32x4*>(src + 4);
         }
     };
+    // (row, 8-dim chunk) items per pass: BLOCK_M*8 of them; a workgroup with more threads than
+    // items (32-row (1,8)) leaves its upper half idle here.
+    constexpr int EITEMS = BLOCK_M * 8;
+    constexpr int EPASS = (EITEMS + NT - 1) / NT;
+    static_assert(EITEMS % NT == 0 || NT % EITEMS == 0, "epilogue items must tile the workgroup");
 #pragma unroll
-    for (int pass = 0; pass < (BLOCK_M * 8) / NT; ++pass) {
+    for (int pass = 0; pass < EPASS; ++pass) {
         const int idx = pass * NT + tid;
+        if (EITEMS < NT && idx >= EITEMS) continue;
         const int row = idx >> 3;
         const int c8 = (idx & 7) * 8;
         const int q = q_base + row;
@@ -908,8 +914,9 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
         STAMP(5);
         if (*last_word) {
 #pragma unroll
-            for (int pass = 0; pass < (BLOCK_M * 8) / NT; ++pass) {
+            for (int pass = 0; pass < EPASS; ++pass) {
                 const int idx = pass * NT + tid;
+                if (EITEMS < NT && idx >= EITEMS) continue;
                 const int row = idx >> 3;
                 const int c8 = (idx & 7) * 8;
                 const int q = q_base + row;
@@ -1088,6 +1095,7 @@ hipError_t launch_fwd_shape(const FwdArgs& a, int grid, int qw, int kw, int rb, 
             case 64 + 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2, 1, true>(a, grid, stream);
             case 128 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 2, true>(a, grid, stream);
             case 64 + 2 * 8 + 4: return launch_fwd<TIn, TOut, 2, 4, 1, true>(a, grid, stream);
+            case 64 + 1 * 8 + 8: return launch_fwd<TIn, TOut, 1, 8, 1, true>(a, grid, stream);
             default: return hipErrorInvalidValue;
         }
     }
@@ -1097,6 +1105,8 @@ hipError_t launch_fwd_shape(const FwdArgs& a, int grid, int qw, int kw, int rb, 
         case 64 + 1 * 8 + 2: return launch_fwd<TIn, TOut, 1, 2, 1, false>(a, grid, stream);
         case 64 + 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2, 1, false>(a, grid, stream);
         case 64 + 2 * 8 + 4: return launch_fwd<TIn, TOut, 2, 4, 1, false>(a, grid, stream);
+        case 64 + 1 * 8 + 4: return launch_fwd<TIn, TOut, 1, 4, 1, false>(a, grid, stream);
+        case 64 + 1 * 8 + 8: return launch_fwd<TIn, TOut, 1, 8, 1, false>(a, grid, stream);
         case 128 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 2, false>(a, grid, stream);
         default: return hipErrorInvalidValue;
     }
@@ -1114,7 +1124,7 @@ hipError_t launch_combine(const CombineArgs& c, hipStream_t stream) {
 bool valid_shape(int qw, int kw, int rb) {
     if (rb == 2) return qw == 2 && kw == 2;
     return rb == 1 && ((qw == 4 && kw == 1) || (qw == 2 && kw == 2) || (qw == 1 && kw == 2) || (qw == 4 && kw == 2) ||
-                       (qw == 2 && kw == 4));
+                       (qw == 2 && kw == 4) || (qw == 1 && kw == 4) || (qw == 1 && kw == 8));
 }
 
 unsigned long long* g_stamps = nullptr;  // diagnostic builds (MHA_STAMPS) only
@@ -1227,19 +1237,29 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
         } else {
             qw = 2;
             kw = 2;
-            // A launch that needs a KV split: one 256-key super-tile per split (the (2,4) shape:
-            // the shortest per-workgroup chain) while that grid stays within one residency round
-            // (2 workgroups per CU by LDS).
-            long g64 = 0, wgs = 0;
-            bool fits = true;
+            // A launch that does not fill the chip with 64-row blocks: one super-tile per split
+            // (single-stage LDS ring, straight-line body) while the grid stays within one
+            // residency round. First choice (1,8): 32 rows x 512 keys per workgroup (128 KiB
+            // LDS, one workgroup per CU, <= 256 of them): half the splits of (2,4), so half the
+            // partial round trip; else (2,4): 64 rows x 256 keys (72 KiB, two per CU, <= 512).
+            long g64 = 0, wgs4 = 0, wgs8 = 0;
+            bool fits4 = true, fits8 = true;
             for (int i = 0; i < n; ++i) {
-                const long g = (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 63) / 64);
-                const long st = (calls[i].nkv + 255) / 256;
-                fits = fits && st <= kMaxSplits;
+                const long b = (long)calls[i].batch * calls[i].heads;
+                const long g = b * ((calls[i].nq + 63) / 64);
+                const long st4 = (calls[i].nkv + 255) / 256, st8 = (calls[i].nkv + 511) / 512;
+                fits4 = fits4 && st4 <= kMaxSplits;
+                fits8 = fits8 && st8 <= kMaxSplits;
                 g64 += g;
-                wgs += g * st;
+                wgs4 += g * st4;
+                wgs8 += b * ((calls[i].nq + 31) / 32) * st8;
             }
-            if (g64 < 256 && fits && wgs <= 512) kw = 4;
+            if (g64 < 256 && fits8 && wgs8 <= 256) {
+                qw = 1;
+                kw = 8;
+            } else if (g64 < 256 && fits4 && wgs4 <= 512) {
+                kw = 4;
+            }
         }
     }
     p.q_waves = qw;
@@ -1251,13 +1271,13 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
         groups += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + block_m - 1) / block_m);
     int want = force_splits > 0 ? force_splits : (int)std::max(1L, (256 + groups - 1) / std::max(1L, groups));
     want = std::max(1, std::min(want, kMaxSplits));
-    if (kw == 4) {
-        // single-super-tile shape: every split must be exactly one super-tile (its LDS ring has
-        // one stage); otherwise (too many keys, or no workspace for the partials) use (2,2).
+    if (kw >= 4) {
+        // single-super-tile shapes: every split must be exactly one super-tile (their LDS ring
+        // has one stage); otherwise (too many keys, or no workspace for the partials) use (2,2).
         size_t off = 0;
         bool ok = true;
         for (int i = 0; i < n; ++i) {
-            const int super_total = std::max(1, (calls[i].nkv + 255) / 256);
+            const int super_total = std::max(1, (calls[i].nkv + 64 * kw - 1) / (64 * kw));
             ok = ok && super_total <= kMaxSplits;
             p.splits[i] = super_total;
             p.tiles_per_split[i] = 1;

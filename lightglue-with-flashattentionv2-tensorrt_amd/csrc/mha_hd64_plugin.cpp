@@ -370,8 +370,8 @@ int32_t mha_hd64_launch_forced(const void* q, const void* k, const void* v, void
     const mha_hd64::Call c{q, k, v, o, batch, heads, nq, nkv};
     const mha_hd64::LaunchPlan plan = mha_hd64::plan_call(c, workspace ? ws_bytes : 0, q_waves, kv_waves, splits);
     const int plan_qw = plan.q_waves + (plan.rows_per_wave == 64 ? 10 : 0);
-    // (2,4) takes one split per 256-key super-tile and falls back to (2,2) past 16 of them
-    const bool single_tile = q_waves == 2 && kv_waves == 4;
+    // (2,4), (1,4), (1,8) take one split per super-tile and fall back to (2,2) past 16 of them
+    const bool single_tile = kv_waves >= 4;
     const bool fell_back = single_tile && plan_qw == 2 && plan.kv_waves == 2;
     if (q_waves != 0 && !fell_back && (plan_qw != q_waves || plan.kv_waves != kv_waves))
         return fail(MHA_HD64_STATUS_BAD_PARAM, __FILE__, __LINE__, "forced workgroup shape is not compiled");

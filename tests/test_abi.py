@@ -215,7 +215,7 @@ def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
     qw, kw, splits, tps = list(out)
     wgs = (1024 // (32 * qw)) * 4 * splits
     assert need <= 5242880 and wgs >= 128 and splits >= 2
-    assert (qw, kw, tps) == (2, 4, 1)  # one 256-key super-tile per split
+    assert (qw, kw, tps) == (1, 8, 1)  # one 512-key super-tile per split
     # max length still fits
     need = lib.mha_hd64_plan(1, 4, 2048, 2048, 5242880, out)
     assert need <= 5242880

@@ -79,9 +79,10 @@ def test_fp16in_fp32out_launcher(name, dev):
 
 # ---- every launch plan (query-wave split x cross-workgroup KV split) against the C oracle ----
 PLAN_SHAPES = [(1, 1), (33, 65), (100, 100), (64, 2048), (300, 129), (1024, 1024), (257, 1000), (16, 4500)]
-# 12 = two 32-row query blocks per wave, 2 q-waves; (2, 4) = one 256-key super-tile per split
-# (the split count follows from nkv; past 16 super-tiles the planner falls back to (2, 2))
-WG_SHAPES = [(4, 1), (2, 2), (1, 2), (4, 2), (12, 2), (2, 4)]
+# 12 = two 32-row query blocks per wave, 2 q-waves; (2, 4), (1, 4), (1, 8) = one super-tile of
+# 64*kv_waves keys per split (the split count follows from nkv; past 16 super-tiles the planner
+# falls back to (2, 2))
+WG_SHAPES = [(4, 1), (2, 2), (1, 2), (4, 2), (12, 2), (2, 4), (1, 4), (1, 8)]
 
 
 @pytest.mark.parametrize("nq,nkv", PLAN_SHAPES)
@@ -92,8 +93,8 @@ def test_forced_plans_match_oracle(nq, nkv, wg, splits, dev, oracle_mod):
 
     q_waves, kv_waves = wg
     super_total = -(-nkv // (64 * kv_waves))
-    if kv_waves == 4 and splits != 1:
-        pytest.skip("(2, 4) takes one split per super-tile")
+    if kv_waves >= 4 and splits != 1:
+        pytest.skip("single-super-tile shapes take one split per super-tile")
     if splits > super_total:
         pytest.skip("more splits than key tiles")
     if -(-super_total // -(-super_total // splits)) != splits:
@@ -345,7 +346,8 @@ def test_grouped_matches_single_calls_bitwise_when_plans_agree(dev):
 # ---- in-launch split combine (arrival tickets; csrc/mha_hd64_kernels.hip epilogue) ----
 FUSED_SHAPES = [  # (nq, nkv, q_waves, kv_waves, splits)
     (1024, 1024, 2, 4, 0), (1024, 1024, 2, 2, 4), (300, 2048, 2, 2, 3), (100, 1000, 12, 2, 3),
-    (64, 4000, 2, 4, 0), (33, 65, 4, 1, 2), (257, 1000, 4, 2, 2)]
+    (64, 4000, 2, 4, 0), (33, 65, 4, 1, 2), (257, 1000, 4, 2, 2), (1024, 1024, 1, 8, 0), (300, 2000, 1, 8, 0),
+    (100, 1000, 1, 4, 0)]
 
 
 def _forced(lib, q, k, v, o, nq, nkv, qw, kw, sp, ws, stream=None):

@@ -13,7 +13,8 @@ from lightglue_amd import _lib, synth  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 SHAPES = [(1024, 1024, 2, 4, 0), (1024, 1024, 2, 2, 4), (300, 2048, 2, 2, 3), (100, 1000, 12, 2, 3),
-          (64, 4000, 2, 4, 0), (33, 65, 4, 1, 2), (257, 1000, 4, 2, 2)]
+          (64, 4000, 2, 4, 0), (33, 65, 4, 1, 2), (257, 1000, 4, 2, 2), (1024, 1024, 1, 8, 0), (300, 2000, 1, 8, 0),
+          (100, 1000, 1, 4, 0)]
 
 
 def main():
