@@ -28,7 +28,9 @@
  *
  * Threading: the plugin object is stateless apart from its namespace string.
  * Concurrent enqueues on different streams are safe when their workspaces
- * differ (same rule as the reference, .cpp:172-175).
+ * differ (same rule as the reference, .cpp:172-175). The library keeps one
+ * small arrival-ticket array per (device, stream) and a per-device arena for
+ * launches recorded under stream capture (see mha_hd64_enqueue).
  */
 #ifndef MHA_HD64_H
 #define MHA_HD64_H
@@ -133,8 +135,13 @@ size_t mha_hd64_get_workspace_size(const mha_hd64_plugin_t* p,
  *   HALF  -> fp16 in, fp32 accumulation, fp16 out   (reference: pad -> fp16in_fp16out kernel -> unpad)
  *   FLOAT -> fp32 in rounded to fp16 (RN) on load, fp32 accumulation, fp32 out
  *            (reference: convert+pad -> fp16in_fp32out kernel -> unpad)
- * One or two kernel launches on `stream`, no host sync. `workspace` must hold
- * mha_hd64_get_workspace_size() bytes. Returns a status. */
+ * One kernel launch on `stream`. A call whose keys are split across workgroups merges the
+ * splits inside that launch through library-owned arrival tickets; the first enqueue on a
+ * (device, stream) outside stream capture allocates them (and, once per device, a pre-zeroed
+ * arena for captured launches, with one stream sync). Without tickets (first use of a stream
+ * inside a capture, env MHA_HD64_FUSED_COMBINE=0) a second, combine kernel does the merge; the
+ * results are bitwise identical. `workspace` must hold mha_hd64_get_workspace_size() bytes.
+ * Returns a status. */
 int32_t mha_hd64_enqueue(mha_hd64_plugin_t* p,
                          const mha_hd64_tensor_desc_t* in, const mha_hd64_tensor_desc_t* out,
                          const void* const* inputs, void* const* outputs,
@@ -165,8 +172,8 @@ size_t mha_hd64_launch_workspace_bytes(int32_t batch, int32_t heads, int32_t nq,
  * image 1 (lightglue_pytorch_with_plugin/lightglue.py:137-152, Nq = Nkv = N0 and N1) and the
  * two CrossBlock directions (lightglue.py:188-205, N0 x N1 and N1 x N0); the reference runs
  * each as its own plugin enqueue (four kernel chains per layer, TransformerLayer :216-226).
- * Up to 4 calls share one main-kernel launch (+ one combine launch when a call splits its
- * keys); longer lists are chunked. All calls use one dtype pair:
+ * Up to 4 calls share one launch (split keys are merged inside it, as for enqueue); longer
+ * lists are chunked. All calls use one dtype pair:
  *   in_type HALF  -> fp16 inputs; FLOAT -> fp32 inputs rounded to fp16 on load
  *   out_type HALF -> fp16 output; FLOAT -> fp32 output
  * Same per-call layout rules as the L0 launchers. Returns a status. */

@@ -13,6 +13,7 @@ from .plugin import (  # noqa: F401
     mha_hd64_batched,
     mha_hd64_grouped,
 )
+from . import ops  # noqa: F401,E402  (registers torch.ops.lightglue_amd.*)
 
 __all__ = [
     "Attention",

@@ -34,7 +34,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib, synth
-from .plugin import PluginError, _check, _workspace, mha_hd64_grouped
+from .plugin import PluginError, _check, _workspace
 
 AttnFn = Callable[[Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]], List[torch.Tensor]]
 
@@ -112,7 +112,8 @@ def _kernel_attention(calls):
     for q, _, _ in calls:
         if not q.is_cuda:
             raise PluginError("LightGlueMatcher: the attention op runs on the GPU only (no CPU fallback)")
-    return mha_hd64_grouped(calls)
+    qs, ks, vs = (list(t) for t in zip(*calls))
+    return torch.ops.lightglue_amd.mha_hd64_grouped(qs, ks, vs)  # ops.py: grouped launches
 
 
 class FourierPositionalEncoding(nn.Module):

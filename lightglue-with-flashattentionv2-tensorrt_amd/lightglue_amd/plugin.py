@@ -341,7 +341,7 @@ class MHAHeadDim64(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, query, key, value):
-        return mha_hd64(query, key, value)
+        return torch.ops.lightglue_amd.mha_hd64(query, key, value)  # ops.py: enqueue on the current stream
 
 
 class Attention(nn.Module):
