@@ -19,20 +19,35 @@ def short(name):
 
 def main():
     kernels = defaultdict(list)
+    intervals = defaultdict(list)
     counters = defaultdict(lambda: defaultdict(list))
     for d in sys.argv[1:]:
         for path in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
             with open(path) as f:
-                for row in csv.DictReader(f):
-                    kernels[row["Kernel_Name"]].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+                rows = sorted(csv.DictReader(f), key=lambda r: int(r["Start_Timestamp"]))
+            for i, row in enumerate(rows):
+                t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
+                kernels[row["Kernel_Name"]].append(t1 - t0)
+                # dispatch-to-dispatch interval inside back-to-back runs of one kernel (graph
+                # replays): the quantity bench.py's event timing of K launches measures
+                if i and rows[i - 1]["Kernel_Name"] == row["Kernel_Name"]:
+                    gap = t0 - int(rows[i - 1]["Start_Timestamp"])
+                    if gap < 3 * (t1 - t0) + 5000:
+                        intervals[row["Kernel_Name"]].append(gap)
         for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(path) as f:
                 for row in csv.DictReader(f):
                     counters[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
     out = {"kernel_trace": {}, "pmc": {}}
     for k, v in sorted(kernels.items(), key=lambda kv: -sum(kv[1])):
-        out["kernel_trace"][short(k)] = {"calls": len(v), "avg_ns": round(statistics.mean(v), 1),
-                                         "median_ns": statistics.median(v), "min_ns": min(v)}
+        e = {"calls": len(v), "avg_ns": round(statistics.mean(v), 1), "median_ns": statistics.median(v),
+             "min_ns": min(v)}
+        iv = intervals.get(k)
+        if iv:
+            e["back_to_back_launches"] = len(iv)
+            e["dispatch_interval_avg_ns"] = round(statistics.mean(iv), 1)
+            e["dispatch_interval_median_ns"] = statistics.median(iv)
+        out["kernel_trace"][short(k)] = e
     for k, cs in counters.items():
         e = {c: {"mean": round(statistics.mean(v), 2), "n": len(v)} for c, v in sorted(cs.items())}
         if "FETCH_SIZE" in cs:
