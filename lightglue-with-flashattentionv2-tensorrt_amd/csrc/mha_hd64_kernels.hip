@@ -303,6 +303,37 @@ __device__ __forceinline__ f32x4 split_scale(f32x4 acc, float inv) {
 #pragma clang fp contract(off)
     return acc * inv;
 }
+// 4-dim forms (workgroups with more threads than (row, 8-dim) items split rows into 16 chunks)
+template <typename T> struct Raw4;
+template <> struct Raw4<f16> { f16x4 x; };
+template <> struct Raw4<float> { f32x4 a; };
+template <int AUX>
+__device__ __forceinline__ void bload4_aux(Raw4<f16>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff) {
+    r.x = __builtin_bit_cast(f16x4, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 0, AUX));
+}
+template <int AUX>
+__device__ __forceinline__ void bload4_aux(Raw4<float>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff) {
+    r.a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, AUX));
+}
+__device__ __forceinline__ f32x4 raw4_to_f32(const Raw4<f16>& r) {
+    return f32x4{(float)r.x[0], (float)r.x[1], (float)r.x[2], (float)r.x[3]};
+}
+__device__ __forceinline__ f32x4 raw4_to_f32(const Raw4<float>& r) { return r.a; }
+template <typename T, int AUX>
+__device__ __forceinline__ void store4b(__amdgpu_buffer_rsrc_t rs, unsigned voff, f32x4 a) {
+    if constexpr (sizeof(T) == 2) {
+        const f16x4 h = f16x4{(f16)a[0], (f16)a[1], (f16)a[2], (f16)a[3]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), rs, voff, 0, AUX);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), rs, voff, 0, AUX);
+    }
+}
+// DPT dims of one row (DPT = 8: a0 = dims 0-3, a1 = 4-7; DPT = 4: a0 only)
+template <typename T, int DPT, int AUX>
+__device__ __forceinline__ void store_dims(__amdgpu_buffer_rsrc_t rs, unsigned voff, f32x4 a0, f32x4 a1) {
+    if constexpr (DPT == 8) store8<T, AUX>(rs, voff, a0, a1);
+    else store4b<T, AUX>(rs, voff, a0);
+}
 __device__ __forceinline__ void raw8_to_f32(const Raw8<f16>& r, f32x4& lo, f32x4& hi) {
     lo = f32x4{(float)r.x[0], (float)r.x[1], (float)r.x[2], (float)r.x[3]};
     hi = f32x4{(float)r.x[4], (float)r.x[5], (float)r.x[6], (float)r.x[7]};
@@ -841,8 +872,17 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     const bool fused = a.tickets != nullptr && ca.splits > 1;
     const __amdgpu_buffer_rsrc_t pml_rs =
         make_rsrc(ca.part_ml + (size_t)bh * ca.splits * nq, (unsigned)(ca.splits * nq * sizeof(float2)));
-    // merge of the KW key-wave partials of (row, dims c8..c8+7) staged in LDS
-    auto merge_waves = [&](int row, int c8, float& M, float& L, f32x4& acc0, f32x4& acc1) {
+    // Epilogue items: (row, chunk of DPT dims). DPT = 8 while a pass has no more threads than
+    // items; workgroups with twice as many threads as 8-dim items (32-row (1,8)) use 4-dim chunks
+    // so every thread merges and stores.
+    constexpr int DPT = BLOCK_M * 8 >= NT ? 8 : 4;
+    constexpr int CPR = kHeadDim / DPT;  // chunks per row
+    constexpr int EITEMS = BLOCK_M * CPR;
+    constexpr int EPASS = (EITEMS + NT - 1) / NT;
+    static_assert(EITEMS % NT == 0, "epilogue items must tile the workgroup");
+    using RawD = typename std::conditional<DPT == 8, Raw8<TOut>, Raw4<TOut>>::type;
+    // merge of the KW key-wave partials of (row, dims c..c+DPT-1) staged in LDS
+    auto merge_waves = [&](int row, int c, float& M, float& L, f32x4& acc0, f32x4& acc1) {
         M = -INFINITY;
         float2 ml[KW];
 #pragma unroll
@@ -857,44 +897,40 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
         for (int k = 0; k < KW; ++k) {
             const float w = (ml[k].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[k].x - M);
             L += w * ml[k].y;
-            const float* src = ol + (k * BLOCK_M + row) * OROW + c8;
+            const float* src = ol + (k * BLOCK_M + row) * OROW + c;
             acc0 += w * *reinterpret_cast<const f32x4*>(src);
-            acc1 += w * *reinterpret_cast<const f32x4*>(src + 4);
+            if constexpr (DPT == 8) acc1 += w * *reinterpret_cast<const f32x4*>(src + 4);
         }
     };
-    // (row, 8-dim chunk) items per pass: BLOCK_M*8 of them; a workgroup with more threads than
-    // items (32-row (1,8)) leaves its upper half idle here.
-    constexpr int EITEMS = BLOCK_M * 8;
-    constexpr int EPASS = (EITEMS + NT - 1) / NT;
-    static_assert(EITEMS % NT == 0 || NT % EITEMS == 0, "epilogue items must tile the workgroup");
 #pragma unroll
     for (int pass = 0; pass < EPASS; ++pass) {
         const int idx = pass * NT + tid;
-        if (EITEMS < NT && idx >= EITEMS) continue;
-        const int row = idx >> 3;
-        const int c8 = (idx & 7) * 8;
+        const int row = idx / CPR;
+        const int chunk = idx % CPR;
+        const int c = chunk * DPT;
         const int q = q_base + row;
         float M, L;
         f32x4 acc0, acc1;
-        merge_waves(row, c8, M, L, acc0, acc1);
+        merge_waves(row, c, M, L, acc0, acc1);
         if (q < nq && !(MHA_ABL & ABL_NO_STORE)) {
             if (ca.splits == 1) {
                 const float inv = 1.f / L;
-                store8<TOut, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c8) * sizeof(TOut)), acc0 * inv, acc1 * inv);
+                store_dims<TOut, DPT, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)), acc0 * inv,
+                                                  acc1 * inv);
             } else {
                 // Partial O_s / l_s in the output precision (fp16 halves the partial traffic of
                 // the fp16 path; the fp32-output path keeps fp32), merged with weights l_s·2^(m_s-M).
                 const unsigned prow = (unsigned)(split * nq + q);
                 const float inv = (L > 0.f) ? 1.f / L : 0.f;
-                const unsigned poff = prow * (unsigned)(kHeadDim * sizeof(TOut)) + c8 * (unsigned)sizeof(TOut);
+                const unsigned poff = prow * (unsigned)(kHeadDim * sizeof(TOut)) + c * (unsigned)sizeof(TOut);
                 if (fused) {
-                    store8<TOut, kSC1>(po_rs, poff, acc0 * inv, acc1 * inv);
-                    if (c8 == 0)
+                    store_dims<TOut, DPT, kSC1>(po_rs, poff, acc0 * inv, acc1 * inv);
+                    if (chunk == 0)
                         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(M, L)), pml_rs,
                                                               prow * (unsigned)sizeof(float2), 0, kSC1);
                 } else {
-                    store8<TOut, MHA_PART_AUX>(po_rs, poff, acc0 * inv, acc1 * inv);
-                    if (c8 == 0) ca.part_ml[((size_t)bh * ca.splits) * nq + prow] = make_float2(M, L);
+                    store_dims<TOut, DPT, MHA_PART_AUX>(po_rs, poff, acc0 * inv, acc1 * inv);
+                    if (chunk == 0) ca.part_ml[((size_t)bh * ca.splits) * nq + prow] = make_float2(M, L);
                 }
             }
         }
@@ -916,23 +952,23 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
 #pragma unroll
             for (int pass = 0; pass < EPASS; ++pass) {
                 const int idx = pass * NT + tid;
-                if (EITEMS < NT && idx >= EITEMS) continue;
-                const int row = idx >> 3;
-                const int c8 = (idx & 7) * 8;
+                const int row = idx / CPR;
+                const int c = (idx % CPR) * DPT;
                 const int q = q_base + row;
                 if (q >= nq) continue;
                 // every split's partial as stored (its own too), merged in split order exactly as
                 // the combine kernel does: the result does not depend on which split came last
                 float2 ml[kMaxSplits];
-                Raw8<TOut> pv[kMaxSplits];
+                RawD pv[kMaxSplits];
 #pragma unroll
                 for (int s2 = 0; s2 < kMaxSplits; ++s2) {
                     if (s2 < ca.splits) {
                         const unsigned prow = (unsigned)(s2 * nq + q);
                         ml[s2] = __builtin_bit_cast(
                             float2, __builtin_amdgcn_raw_buffer_load_b64(pml_rs, prow * (unsigned)sizeof(float2), 0, kSC1));
-                        bload8_aux<kSC1>(pv[s2], po_rs,
-                                         prow * (unsigned)(kHeadDim * sizeof(TOut)) + c8 * (unsigned)sizeof(TOut));
+                        const unsigned off = prow * (unsigned)(kHeadDim * sizeof(TOut)) + c * (unsigned)sizeof(TOut);
+                        if constexpr (DPT == 8) bload8_aux<kSC1>(pv[s2], po_rs, off);
+                        else bload4_aux<kSC1>(pv[s2], po_rs, off);
                     }
                 }
                 float Mt = -INFINITY;
@@ -946,16 +982,20 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
                     if (s2 < ca.splits) {
                         const float w = split_weight(ml[s2], Mt);
                         L += w;
-                        f32x4 lo, hi;
-                        raw8_to_f32(pv[s2], lo, hi);
-                        split_accumulate(acc0, w, lo);
-                        split_accumulate(acc1, w, hi);
+                        if constexpr (DPT == 8) {
+                            f32x4 lo, hi;
+                            raw8_to_f32(pv[s2], lo, hi);
+                            split_accumulate(acc0, w, lo);
+                            split_accumulate(acc1, w, hi);
+                        } else {
+                            split_accumulate(acc0, w, raw4_to_f32(pv[s2]));
+                        }
                     }
                 }
                 const float inv = 1.f / L;
                 if (!(MHA_ABL & ABL_NO_STORE))
-                    store8<TOut, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c8) * sizeof(TOut)),
-                                             split_scale(acc0, inv), split_scale(acc1, inv));
+                    store_dims<TOut, DPT, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)),
+                                                      split_scale(acc0, inv), split_scale(acc1, inv));
             }
         }
     }
