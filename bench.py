@@ -433,22 +433,36 @@ def main():
         # dispatch-to-dispatch interval, an upper bound on the kernel's own duration). The production
         # form is ONE launch (split partials merged by each query group's last-arriving workgroup);
         # the two-kernel form (main + combine kernel) is timed beside it.
+        direct = q_waves == 21  # the single-pass kernel (csrc/mha_hd64_direct.hip)
         t_main = graph_per_launch_ms(torch, lambda: forced(3), stream)
+
+        # The ring kernel's split plan for the same call, timed beside the production kernel: (1,8)
+        # with the 2-way split merged in-launch, and its two-kernel form (main + combine kernel).
+        def ring(mask):
+            lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), 1, 4, nq, nkv, 0,
+                                       0, 1, 8, 0, ws_buf2.data_ptr(), ws_buf2.numel(),
+                                       torch.cuda.current_stream(device).cuda_stream, mask)
+
+        ws_buf2 = torch.empty(5242880, dtype=torch.uint8, device=device)
+        t_ring = graph_per_launch_ms(torch, lambda: ring(3), stream)
         lib.mha_hd64_set_fused_combine(0)
-        t_main2 = graph_per_launch_ms(torch, lambda: forced(1), stream)
-        t_comb2 = graph_per_launch_ms(torch, lambda: forced(2), stream) if splits > 1 else 0.0
-        t_two = graph_per_launch_ms(torch, lambda: forced(3), stream)
+        t_main2 = graph_per_launch_ms(torch, lambda: ring(1), stream)
+        t_comb2 = graph_per_launch_ms(torch, lambda: ring(2), stream)
+        t_two = graph_per_launch_ms(torch, lambda: ring(3), stream)
         lib.mha_hd64_set_fused_combine(1)
         t_call = statistics.median(event_durations_ms(torch, full_call, 200, stream)[20:])
         achieved = flops / (t_main * 1e-3) / 1e12
-        traffic = load_traffic("main_kernel_bytes_per_launch")
+        traffic = load_traffic("direct_kernel_bytes_per_launch" if direct else "main_kernel_bytes_per_launch")
+        kname = ("mha_hd64_direct_kernel<f16,TPW=2> (single pass: 32 query rows x all keys per workgroup, "
+                 "no split)" if direct else
+                 f"mha_hd64_fwd_kernel<f16,f16,{q_waves},{kv_waves}> ({splits}-way KV split, in-launch combine)")
         result["roofline"] = {
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": traffic,
-            "kernel": f"mha_hd64_fwd_kernel<f16,f16,{q_waves},{kv_waves}> ({splits}-way KV split, in-launch combine)",
+            "kernel": kname,
             "kernel_us": round(t_main * 1e3, 3),
-            "two_kernel_form_us": {"main": round(t_main2 * 1e3, 3), "combine": round(t_comb2 * 1e3, 3),
-                                   "both": round(t_two * 1e3, 3)},
+            "ring_split_plan_us": {"in_launch_combine": round(t_ring * 1e3, 3), "main": round(t_main2 * 1e3, 3),
+                                   "combine": round(t_comb2 * 1e3, 3), "two_kernels": round(t_two * 1e3, 3)},
             "timing": "graph replay of 200 back-to-back launches per kernel on the launch stream",
             "flops_per_launch": flops, "algorithmic_bytes_per_call": call_bytes(1, 4, nq, nkv),
         }

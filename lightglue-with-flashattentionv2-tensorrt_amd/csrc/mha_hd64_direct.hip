@@ -1,0 +1,306 @@
+// mha_hd64_direct.hip — single-pass FlashAttention forward, head_dim = 64, for gfx950 (MI355X).
+//
+// The same operator as mha_hd64_kernels.hip (O = softmax(Q·Kᵀ·0.125)·V per (batch, head); the
+// reference's attention_headdim_64_fp16in_fp16out.cu:253-733 / …fp16in_fp32out.cu:253-703), laid
+// out for launches that cannot fill the chip with query blocks alone — the plugin's single
+// 1x4x1024x1024 call is 128 blocks of 32 rows.
+//
+// The LDS-ring kernel fills 256 CUs there by splitting each query block's keys over two
+// workgroups and merging the two partials through L2 (publish, ticket, read back: ≈ 1.7 µs of
+// dependent round trips per call). This kernel gives ONE workgroup all the keys of its 32-row
+// query block instead: 8 waves, wave w owns keys [64·TPW·w, 64·TPW·(w+1)), so no other workgroup
+// ever needs its partial and the merge is an LDS exchange between the 8 waves.
+//  * Nothing is shared between waves until the epilogue, so nothing is staged for sharing: every
+//    wave loads its own K straight into MFMA A-operand registers (K rows on lanes), and its own V
+//    through a wave-private LDS image (the transposing ds_read_b64_tr_b16 needs V in LDS), with no
+//    barrier before the epilogue. All loads are issued up front (Q, K tile by tile, then V), so
+//    QKᵀ of the first tile starts as soon as its K lands while the rest streams in.
+//  * Per tile (64 keys): Sᵀ = K·Qᵀ on v_mfma_f32_32x32x16_f16 with the running max and the tail
+//    mask folded into a bias k-step, one v_exp_f32 per probability, P packed to fp16 as the B
+//    operand of Oᵀ = Vᵀ·Pᵀ, row sums on a 16x16x32 MFMA, lazy rescale (threshold 8 in log2
+//    units) — the arithmetic of the ring kernel's step, so both kernels agree to rounding.
+//  * Epilogue: each wave stages Oᵀ (fp32, at its own max) and (m, l) in its own LDS region; one
+//    barrier; 512 threads merge (row, 4 dims) over the 8 waves and store O.
+// The planner (plan_group) picks this kernel for fp16 inputs when nkv <= 1024 and the launch has
+// at most 256 such workgroups (one residency round); everything else runs the ring kernel.
+#include <hip/hip_runtime.h>
+
+#include "mha_hd64_device.h"
+#include "mha_hd64_internal.h"
+
+namespace mha_hd64 {
+namespace {
+
+template <typename TOut, int TPW, bool MULTI>
+__global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
+    constexpr int KW = 8;                               // waves (key slices) per workgroup
+    constexpr int BLOCK_M = 32;                         // query rows per workgroup
+    constexpr int WAVE_KEYS = kTileKV * TPW;            // keys per wave
+    constexpr int OROW = 68;                            // epilogue fp32 row pitch (64 dims + 4 pad)
+    constexpr int EPI_WAVE = BLOCK_M * OROW * 4;        // one wave's staged Oᵀ
+    // Wave-private region: the wave's V tiles, later its staged Oᵀ (8704 = 68 x 128 B keeps the
+    // bank phase of every region the same as a region at 0).
+    constexpr int RS = TPW * kTileBytes > EPI_WAVE ? TPW * kTileBytes : EPI_WAVE;
+    constexpr int LDS_BYTES = KW * RS + KW * BLOCK_M * 2 * 4;
+    static_assert(RS % 128 == 0 && LDS_BYTES <= 160 * 1024, "LDS layout");
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    lds_char* const lds = (lds_char*)smem;
+
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int r = lane & 31;   // query column of the MFMA tiles
+    const int hh = lane >> 5;  // half-wave
+    // XCD-aware order (as the ring kernel): consecutive j share an XCD, so the query blocks of
+    // one (batch, head) read its K/V through one L2.
+    int qtile, bh, j;
+    {
+        const int T = a.total_blocks, L = blockIdx.x;
+        const int q8 = T >> 3, r8 = T & 7, xcd = L & 7;
+        j = xcd * q8 + min(xcd, r8) + (L >> 3);
+    }
+    int ci = 0;
+    if constexpr (MULTI) {
+#pragma unroll
+        for (int i = 1; i < kMaxCalls; ++i) ci += (int)((i < a.n_calls) & (j >= a.c[i].block_begin));
+    }
+    const CallArgs ca = MULTI ? pick_call(a, ci) : a.c[0];
+    {
+        const int jl = j - ca.block_begin;
+        qtile = jl % ca.qtiles;
+        bh = jl / ca.qtiles;
+    }
+    const int nq = ca.nq, nkv = ca.nkv;
+    const f16* Qb = reinterpret_cast<const f16*>(ca.q) + (size_t)bh * nq * kHeadDim;
+    const f16* Kb = reinterpret_cast<const f16*>(ca.k) + (size_t)bh * nkv * kHeadDim;
+    const f16* Vb = reinterpret_cast<const f16*>(ca.v) + (size_t)bh * nkv * kHeadDim;
+    const __amdgpu_buffer_rsrc_t q_rs = make_rsrc(Qb, (unsigned)nq * kHeadDim * 2);
+    const __amdgpu_buffer_rsrc_t k_rs = make_rsrc(Kb, (unsigned)nkv * kHeadDim * 2);
+    const __amdgpu_buffer_rsrc_t v_rs = make_rsrc(Vb, (unsigned)nkv * kHeadDim * 2);
+    const int q_row = qtile * BLOCK_M + r;
+    const int key0 = wave * WAVE_KEYS;
+    // tiles of this wave holding at least one key (wave-uniform)
+    const int n_t = max(0, min(TPW, (nkv - key0 + kTileKV - 1) / kTileKV));
+    const unsigned region = (unsigned)wave * RS;
+
+    f32x16 o0 = {}, o1 = {};  // Oᵀ: dims 0..31 / 32..63, query on the lane
+    f32x4 l_acc = {0.f, 0.f, 0.f, 0.f};
+    float m_run = 0.f;
+
+    if (n_t > 0) {
+        // ---- loads, all up front (unconditional: rows past nkv read as zero) ----
+        Raw8<f16> qraw[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if (MHA_ABL & ABL_NO_GLOAD) qraw[s].x = f16x8{} + (f16)(lane * 0.01f);
+            else bload8(qraw[s], q_rs, (unsigned)(q_row * kHeadDim + 16 * s + 8 * hh) * 2, 0);
+        }
+        // K, then V, of this wave's TPW tiles reach LDS by LDS-DMA in whole 128-B rows (1 KiB per
+        // instruction: rows 8i..8i+7), swizzled on the source side (the DMA writes lane-linear):
+        // LDS position p of row `row` receives the 16-B chunk p ^ swz(row) (k_off / v_off images).
+        // K and V take turns in the wave's region: K's fragments are read into registers, then
+        // V lands over them while QKᵀ and the softmax run.
+        auto dma_rows = [&](__amdgpu_buffer_rsrc_t rs, bool is_k) {
+#pragma unroll
+            for (int i = 0; i < 8 * TPW; ++i) {
+                const int row = 8 * i + (lane >> 3), pos = lane & 7;
+                const int ch = is_k ? (pos ^ ((row >> 1) & 7)) : (pos ^ (((row >> 1) & 1) << 2));
+                if (MHA_ABL & ABL_NO_GLOAD) continue;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * i), 16,
+                    (unsigned)((key0 + row) * kHeadDim + ch * 8) * 2, 0, 0, 0);
+            }
+        };
+        dma_rows(k_rs, true);
+        // (the compiler does not order these LDS reads after the DMA: wait for it explicitly)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // K fragments (A operand of Sᵀ = K·Qᵀ): kf[t][2s] = K[64t+r][16s+8hh..+7], kf[t][2s+1] = rows +32
+        f16x8 kf[TPW][8];
+#pragma unroll
+        for (int t = 0; t < TPW; ++t)
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2)
+                    kf[t][2 * s + h2] = lds_read16(lds, region + k_off(kTileKV * t + 32 * h2 + r, 2 * s + hh));
+        // Q fragments (B operand of Sᵀ = K·Qᵀ), scaled by 0.125·log2(e) in fp16.
+        f16x8 qf[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) qf[s][e] = (f16)((float)qraw[s].x[e] * kScaleLog2);
+
+        // every K fragment is in registers before V's DMA overwrites the region; Q is consumed
+        // (scaled) before it too, so no Q use waits behind the V DMA (the compiler drains all
+        // outstanding loads at a plain load's use while an LDS-DMA is in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
+        dma_rows(v_rs, false);
+
+        // Row sums on the matrix pipe and the bias k-step: as the ring kernel (mha_hd64_kernels.hip).
+        const f16 sel = (((lane & 15) >> 2) & 1) == ((lane >> 4) & 1) ? (f16)1.f : (f16)0.f;
+        const f16x8 a_sum = f16x8{sel, sel, sel, sel, sel, sel, sel, sel};
+        const f16 one_h = hh == 0 ? (f16)1.f : (f16)0.f;
+        f16x8 b_bias = f16x8{0, 0, one_h, 0, 0, 0, 0, 0};  // m_run = 0
+        auto set_bias = [&]() {
+            const f16 hi = (f16)(-m_run);
+            const f16 lo = (f16)(-m_run - (float)hi);
+            b_bias = hh == 0 ? f16x8{hi, lo, (f16)1.f, 0, 0, 0, 0, 0} : f16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        };
+        auto a_bias_of = [&](int t, int half) -> f16x8 {
+            const int key = key0 + kTileKV * t + 32 * half + r;
+            const f16 mk = (hh == 0 && key >= nkv) ? (f16)kMaskBias : (f16)0.f;
+            return f16x8{one_h, one_h, mk, 0, 0, 0, 0, 0};
+        };
+        // V tr-read lane addressing (see the ring kernel): rows 4hh+qq (+const), swizzled halves.
+        const int g16 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+        const int vb = (qq >> 1) & 1;
+        const unsigned v_lane = 128 * (4 * hh + qq) + 16 * (2 * (g16 & 1) + (pp >> 1)) + 8 * (pp & 1);
+
+        // Phase 1, while V is still in flight: the probabilities of every tile of the wave. Every
+        // tile runs, even one wholly past nkv (its keys are masked: P = 0 and the max does not
+        // move), so no branch separates the up-front loads from their uses.
+        f16x8 p[TPW][2][2];  // P (fp16) as the B operand: p[t][half][k-step]
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            // Sᵀ = K·Qᵀ - m (bias k-step first), two 32-key halves
+            const bool partial = key0 + kTileKV * (t + 1) > nkv;
+            const f16x8 ab0 = partial ? a_bias_of(t, 0) : f16x8{one_h, one_h, 0, 0, 0, 0, 0, 0};
+            const f16x8 ab1 = partial ? a_bias_of(t, 1) : f16x8{one_h, one_h, 0, 0, 0, 0, 0, 0};
+            const f32x16 zero = {};
+            f32x16 c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab0, b_bias, zero, 0, 0, 0);
+            f32x16 c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab1, b_bias, zero, 0, 0, 0);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (MHA_ABL & ABL_NO_QK) {
+                    keep_live(kf[t][2 * s]);
+                    keep_live(kf[t][2 * s + 1]);
+                    continue;
+                }
+                c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][2 * s], qf[s], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][2 * s + 1], qf[s], c1, 0, 0, 0);
+            }
+            const float mx = xhalf_max(tree_max(c0, c1));
+            // online softmax: the first tile sets the max; a later one moves it only when a query's
+            // tile max exceeds it by > kRescaleThr (wave-uniform branch). No PV has run yet, so a
+            // move rescales the earlier tiles' probabilities instead of O.
+            if (t == 0 || __builtin_amdgcn_ballot_w64(mx > kRescaleThr) != 0) {
+                const float d = t == 0 ? ((mx < kEmptyMax) ? 0.f : mx) : fmaxf(mx, 0.f);
+                if (t > 0) {
+                    const f16 alpha = (f16)__builtin_amdgcn_exp2f(-d);
+#pragma unroll
+                    for (int t2 = 0; t2 < t; ++t2)
+#pragma unroll
+                        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+                            for (int ss = 0; ss < 2; ++ss) p[t2][h2][ss] *= alpha;
+                }
+                m_run += d;
+                c0 -= d;
+                c1 -= d;
+                set_bias();
+            }
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                if (MHA_ABL & ABL_NO_EXP) continue;
+                c0[e] = __builtin_amdgcn_exp2f(c0[e]);
+                c1[e] = __builtin_amdgcn_exp2f(c1[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                p[t][0][0][e] = (f16)c0[e];
+                p[t][0][1][e] = (f16)c0[8 + e];
+                p[t][1][0][e] = (f16)c1[e];
+                p[t][1][1][e] = (f16)c1[8 + e];
+            }
+        }
+        // Phase 2: V has landed (DMA) -> Oᵀ = Vᵀ·Pᵀ and the row sums.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            const unsigned va0 = region + t * kTileBytes + v_lane + 64 * vb;
+            const unsigned va1 = region + t * kTileBytes + v_lane + 64 * (1 - vb);
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    const unsigned rowc = 128 * (32 * jj + 16 * ss);
+                    const f16x8 vfa = cat8(tr_read(lds, va0 + rowc), tr_read(lds, va0 + rowc + 8 * 128));
+                    const f16x8 vfb = cat8(tr_read(lds, va1 + rowc), tr_read(lds, va1 + rowc + 8 * 128));
+                    if (MHA_ABL & ABL_NO_PV) {
+                        keep_live(vfa);
+                        keep_live(vfb);
+                        keep_live(p[t][jj][ss]);
+                        continue;
+                    }
+                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa, p[t][jj][ss], o0, 0, 0, 0);
+                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb, p[t][jj][ss], o1, 0, 0, 0);
+                    l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, p[t][jj][ss], l_acc, 0, 0, 0);
+                }
+        }
+    }
+
+    // ---- epilogue: merge the 8 key slices through LDS ----
+    // The wave's V region is its own, so its staged Oᵀ overwrites only what it has read itself.
+    float* ol = reinterpret_cast<float*>(smem + region);      // [32][OROW]
+    float* mlb = reinterpret_cast<float*>(smem + KW * RS);   // [KW][32][2]
+    {
+        const float L_w = l_acc[0];
+        const float m_w = (L_w > 0.f) ? m_run : -INFINITY;
+        float* dst = ol + r * OROW;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int d = 8 * g4 + 4 * hh;
+            *reinterpret_cast<f32x4*>(dst + d) = f32x4{o0[4 * g4], o0[4 * g4 + 1], o0[4 * g4 + 2], o0[4 * g4 + 3]};
+            *reinterpret_cast<f32x4*>(dst + 32 + d) =
+                f32x4{o1[4 * g4], o1[4 * g4 + 1], o1[4 * g4 + 2], o1[4 * g4 + 3]};
+        }
+        if (hh == 0) *reinterpret_cast<float2*>(mlb + (wave * BLOCK_M + r) * 2) = make_float2(m_w, L_w);
+    }
+    __syncthreads();
+    // thread -> (row, 4 dims): 32 rows x 16 chunks = 512 items
+    const int row = tid >> 4, c = (tid & 15) * 4;
+    const int q = qtile * BLOCK_M + row;
+    float2 ml[KW];
+    float M = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+        ml[k] = *reinterpret_cast<const float2*>(mlb + (k * BLOCK_M + row) * 2);
+        M = fmaxf(M, ml[k].x);
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    float L = 0.f;
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+        const float w = (ml[k].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[k].x - M);
+        L += w * ml[k].y;
+        acc += w * *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(smem + k * RS) + row * OROW + c);
+    }
+    if (q < nq && !(MHA_ABL & ABL_NO_STORE)) {
+        const __amdgpu_buffer_rsrc_t o_rs = make_rsrc(reinterpret_cast<TOut*>(ca.o) + (size_t)bh * nq * kHeadDim,
+                                                      (unsigned)(nq * kHeadDim * sizeof(TOut)));
+        store4b<TOut, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)), acc * (1.f / L));
+    }
+}
+
+template <typename TOut, int TPW>
+hipError_t launch_direct_t(const FwdArgs& a, int grid, hipStream_t stream) {
+    if (a.n_calls > 1)
+        hipLaunchKernelGGL((mha_hd64_direct_kernel<TOut, TPW, true>), dim3(grid), dim3(512), 0, stream, a);
+    else
+        hipLaunchKernelGGL((mha_hd64_direct_kernel<TOut, TPW, false>), dim3(grid), dim3(512), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_direct(const FwdArgs& a, int grid, int tiles_per_wave, bool out_f32, hipStream_t stream) {
+    switch (tiles_per_wave * 2 + (out_f32 ? 1 : 0)) {
+        case 2: return launch_direct_t<f16, 1>(a, grid, stream);
+        case 3: return launch_direct_t<float, 1>(a, grid, stream);
+        case 4: return launch_direct_t<f16, 2>(a, grid, stream);
+        case 5: return launch_direct_t<float, 2>(a, grid, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace mha_hd64

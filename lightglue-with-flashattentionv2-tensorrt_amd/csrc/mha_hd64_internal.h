@@ -36,6 +36,7 @@ struct LaunchPlan {
     int splits;           // KV split across workgroups (1 = no combine pass)
     int tiles_per_split;  // KV super-tiles (64 * kv_waves keys) per split
     size_t ws_needed;     // workspace bytes the plan uses
+    int direct_tiles;     // > 0: single-pass kernel, 8 waves x direct_tiles 64-key tiles (no split)
 };
 
 // Up to kGroupCalls calls share one launch (grouped launcher); larger groups are chunked.
@@ -51,9 +52,12 @@ struct GroupPlan {
     int tiles_per_split[kGroupCalls];
     size_t ws_offset[kGroupCalls];
     size_t ws_needed;
+    int direct_tiles;  // > 0: the single-pass kernel (mha_hd64_direct.hip), q_waves 1 x kv_waves 8
 };
+// force_q_waves = kForceDirect selects the single-pass kernel (fp16 input, nkv <= 1024).
+constexpr int kForceDirect = 21;
 GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_waves = 0, int force_kv_waves = 0,
-                     int force_splits = 0);
+                     int force_splits = 0, InType in = InType::F16);
 hipError_t launch_group(const Call* calls, int n, InType in, OutType out, void* workspace, size_t ws_bytes,
                         hipStream_t stream, int force_q_waves = 0, int force_kv_waves = 0, int force_splits = 0,
                         int phase_mask = 3);
@@ -62,7 +66,7 @@ size_t group_workspace_bytes(const Call* calls, int n);
 // Workgroup shapes compiled: (q_waves, kv_waves) in {(4,1), (2,2), (1,2), (4,2)} with 32-row waves,
 // and (2,2) with 64-row waves (forced as q_waves = 12).
 LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves = 0, int force_kv_waves = 0,
-                     int force_splits = 0);
+                     int force_splits = 0, InType in = InType::F16);
 size_t split_workspace_bytes(const Call& c, int splits);
 
 // Returns hipSuccess or the launch error. phase_mask (measurement hook): bit 0 = main

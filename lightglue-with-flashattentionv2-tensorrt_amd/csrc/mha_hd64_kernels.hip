@@ -44,304 +44,12 @@
 #include <utility>
 #include <vector>
 
+#include "mha_hd64_device.h"
 #include "mha_hd64_internal.h"
 
 namespace mha_hd64 {
 namespace {
 
-typedef _Float16 f16;
-typedef f16 f16x8 __attribute__((ext_vector_type(8)));
-typedef f16 f16x4 __attribute__((ext_vector_type(4)));
-typedef short i16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
-
-constexpr float kScaleLog2 = 0.18033688011112042f;  // 0.125 * log2(e)
-constexpr float kRescaleThr = 8.0f;                  // lazy-rescale threshold (log2 units)
-constexpr int kTileKV = 64;                          // keys per LDS tile
-constexpr int kTileBytes = kTileKV * kHeadDim * 2;   // 8 KiB fp16 tile
-
-// One call of a launch (a launch carries up to kMaxCalls independent calls of any shapes: the
-// grouped launcher runs self0+self1 or cross0->1+cross1->0 of a LightGlue layer as one launch).
-constexpr int kMaxCalls = kGroupCalls;
-constexpr int kMaxSplits = 16;  // KV splits per query group (combine loads them all in one round)
-struct CallArgs {
-    const void* q;
-    const void* k;
-    const void* v;
-    void* o;
-    void* part_o;     // [bh][splits][nq][64] O_s / l_s in TOut precision (splits > 1 only)
-    float2* part_ml;  // [bh][splits][nq] (m in log2 units, l)
-    int nq;
-    int nkv;
-    int splits;
-    int tiles_per_split;
-    int qtiles;       // query blocks per (batch, head)
-    int bh;           // batch * heads
-    int block_begin;  // first block (in XCD-remapped order j) of this call
-    int pad_;
-};
-struct FwdArgs {
-    CallArgs c[kMaxCalls];
-    int n_calls;
-    int total_blocks;            // grid size (kept here so the first scalar-load round has it)
-    unsigned long long* stamps;  // diagnostic builds only (MHA_STAMPS): 8 x u64 per workgroup
-    // In-launch combine (non-null): one arrival ticket per query group, indexed by the group's
-    // first block j; zero between launches (the last arriver resets its ticket).
-    unsigned* tickets;
-};
-
-// Uniform (scalar) selection of call ci's arguments from the kernarg table (grouped launches).
-__device__ __forceinline__ CallArgs pick_call(const FwdArgs& a, int ci) {
-    CallArgs ca = a.c[0];
-#pragma unroll
-    for (int i = 1; i < kMaxCalls; ++i)
-        if (ci == i) ca = a.c[i];
-    return ca;
-}
-
-// LDS images (byte offsets inside one 8 KiB [64 rows][128 B] tile; chunk = 16 B = 8 halfs).
-// K is read row-wise by ds_read_b128 (lane = key row): XOR the chunk with (row>>1)&7
-// so the 16 rows of every b128 lane group hit 16 distinct 16-B bank slots.
-// V is read column-wise by ds_read_b64_tr_b16 (4 rows x 32 cols per half-wave): XOR
-// the chunk with ((row>>1)&1)<<2 so rows r and r+2 use opposite 64-B halves of the bank row.
-__device__ __forceinline__ int k_off(int row, int chunk) {
-    return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
-}
-__device__ __forceinline__ int v_off(int row, int chunk) {
-    return row * 128 + ((chunk ^ (((row >> 1) & 1) << 2)) << 4);
-}
-
-template <typename T> struct Raw8;
-template <> struct Raw8<f16> { f16x8 x; };
-template <> struct Raw8<float> { f32x4 a, b; };
-
-__device__ __forceinline__ void load8(Raw8<f16>& r, const f16* p) {
-    r.x = *reinterpret_cast<const f16x8*>(p);
-}
-__device__ __forceinline__ void load8(Raw8<float>& r, const float* p) {
-    r.a = *reinterpret_cast<const f32x4*>(p);
-    r.b = *reinterpret_cast<const f32x4*>(p + 4);
-}
-__device__ __forceinline__ f16x8 to_f16(const Raw8<f16>& r) { return r.x; }
-__device__ __forceinline__ f16x8 to_f16(const Raw8<float>& r) {
-    // Round-to-nearest-even, as the reference's __float22half2_rn (…fp32out.cu:706-768).
-    const f16x4 lo = __builtin_convertvector(r.a, f16x4);
-    const f16x4 hi = __builtin_convertvector(r.b, f16x4);
-    return f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-}
-
-// Cross-half (lane l <-> l^32) reductions via v_permlane32_swap.
-__device__ __forceinline__ float xhalf_max(float x) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-// Row max of the 32 scores of a lane as a v_max3_f32 tree (16 instructions: 11 + 4 + 1).
-__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
-__device__ __forceinline__ float tree_max(const f32x16& a, const f32x16& b) {
-    float t[11];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) t[i] = max3f(a[3 * i], a[3 * i + 1], a[3 * i + 2]);
-    t[5] = max3f(a[15], b[0], b[1]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) t[6 + i] = max3f(b[2 + 3 * i], b[3 + 3 * i], b[4 + 3 * i]);
-    t[10] = fmaxf(b[14], b[15]);
-    const float u0 = max3f(t[0], t[1], t[2]), u1 = max3f(t[3], t[4], t[5]);
-    const float u2 = max3f(t[6], t[7], t[8]), u3 = fmaxf(t[9], t[10]);
-    return fmaxf(max3f(u0, u1, u2), u3);
-}
-// LDS accesses through an explicit address-space-3 base and 32-bit byte offsets, so the
-// compiler folds the compile-time part of every address into the DS instruction's offset field.
-typedef __attribute__((address_space(3))) char lds_char;
-typedef __attribute__((address_space(3))) f16x8 lds_f16x8;
-
-__device__ __forceinline__ f16x4 tr_read(lds_char* lds, unsigned byte_off) {
-    const i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(lds + byte_off));
-    return __builtin_bit_cast(f16x4, v);
-}
-__device__ __forceinline__ f16x8 lds_read16(lds_char* lds, unsigned byte_off) {
-    return *(lds_f16x8*)(lds + byte_off);
-}
-__device__ __forceinline__ void lds_write16(lds_char* lds, unsigned byte_off, f16x8 v) {
-    *(lds_f16x8*)(lds + byte_off) = v;
-}
-
-__device__ __forceinline__ f16x8 cat8(f16x4 a, f16x4 b) {
-    return f16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-}
-
-template <typename TOut>
-__device__ __forceinline__ void store4(TOut* dst, float a, float b, float c, float d);
-template <>
-__device__ __forceinline__ void store4<float>(float* dst, float a, float b, float c, float d) {
-    *reinterpret_cast<f32x4*>(dst) = f32x4{a, b, c, d};
-}
-template <>
-__device__ __forceinline__ void store4<f16>(f16* dst, float a, float b, float c, float d) {
-    *reinterpret_cast<f16x4*>(dst) = f16x4{(f16)a, (f16)b, (f16)c, (f16)d};
-}
-
-__device__ __forceinline__ f32x16 splat16(float x) {
-    return f32x16{x, x, x, x, x, x, x, x, x, x, x, x, x, x, x, x};
-}
-
-// Diagnostic ablation switches (tools/ablate_build.sh builds each into lib/exp/; the shipped
-// library defines none of them). Results of an ablated build are wrong by construction.
-#ifndef MHA_ABL
-#define MHA_ABL 0
-#endif
-#define ABL_NO_BARRIER 1
-#define ABL_NO_REFILL 2
-#define ABL_NO_EXP 4
-#define ABL_NO_SOFTMAX 8
-#define ABL_NO_PV 16
-#define ABL_NO_QK 32
-#define ABL_NO_GLOAD 64   // no K/V/Q global loads (LDS and Q hold garbage)
-#define ABL_NO_STORE 128  // no output / partial stores
-#define ABL_K_CONST 256   // K fragments from registers (no K LDS reads)
-#define ABL_V_CONST 512   // V fragments from registers (no V LDS reads)
-__device__ __forceinline__ void keep_live(const f16x8& x) { asm volatile("" ::"v"(x)); }
-
-// In-kernel timestamps (diagnostic build -DMHA_STAMPS only): s_memtime after draining memory.
-#ifdef MHA_STAMPS
-#define STAMP(slot)                                                                                       \
-    do {                                                                                                  \
-        __builtin_amdgcn_sched_barrier(0);                                                                \
-        unsigned long long t_;                                                                            \
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-        __builtin_amdgcn_sched_barrier(0);                                                                \
-        if (threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (slot)] = t_;                                     \
-    } while (0)
-#else
-#define STAMP(slot) \
-    do {            \
-    } while (0)
-#endif
-
-#ifndef MHA_ST_AUX
-#define MHA_ST_AUX 0    // cache policy bits of the output stores (2 = nt, 16 = sc1)
-#endif
-#ifndef MHA_PART_AUX
-#define MHA_PART_AUX 0  // cache policy bits of the split-partial stores
-#endif
-
-// Per-step phase clocks (diagnostic build -DMHA_STEPSTAMPS only): s_memtime at phase boundaries
-// of every full loop step, summed per wave, waited for only at the next step's barrier.
-#ifdef MHA_STEPSTAMPS
-#define TCLK(var)                                  \
-    do {                                           \
-        __builtin_amdgcn_sched_barrier(0);         \
-        var = __builtin_readcyclecounter();        \
-        __builtin_amdgcn_sched_barrier(0);         \
-    } while (0)
-#else
-#define TCLK(var) \
-    do {          \
-    } while (0)
-#endif
-
-#ifndef MHA_PINGPONG
-#define MHA_PINGPONG 0  // measured neutral on the steady loop (vector-issue bound), and it makes the
-                        // fp32-input 8-wave kernel spill: off by default, kept as a switch
-#endif
-
-constexpr float kMaskBias = -65504.f;  // fp16 lowest: a masked key's score, exp2 -> 0
-constexpr float kEmptyMax = -30000.f;  // tile max below this: every key of the tile was masked
-
-// Buffer loads (T8): a per-head descriptor whose record count is the head's byte size, so
-// rows past nq / nkv read as zeros in hardware (no clamps, no 64-bit address math per load);
-// the per-iteration key offset rides in the scalar soffset.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
-}
-// 8 consecutive output values (dims c8..c8+7 of one row) as one (f16) or two (f32) 16-B stores.
-template <typename T, int AUX>
-__device__ __forceinline__ void store8(__amdgpu_buffer_rsrc_t rs, unsigned voff, f32x4 a, f32x4 b) {
-    if constexpr (sizeof(T) == 2) {
-        const f16x8 h = f16x8{(f16)a[0], (f16)a[1], (f16)a[2], (f16)a[3], (f16)b[0], (f16)b[1], (f16)b[2], (f16)b[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, h), rs, voff, 0, AUX);
-    } else {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), rs, voff, 0, AUX);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, b), rs, voff + 16, 0, AUX);
-    }
-}
-__device__ __forceinline__ void bload8(Raw8<f16>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff) {
-    r.x = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
-}
-__device__ __forceinline__ void bload8(Raw8<float>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff) {
-    r.a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
-    r.b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16, soff, 0));
-}
-// cache-policy bits of the buffer intrinsics' aux operand: sc1 (write-through store / L1-bypassing
-// load; the inter-workgroup hand-off form of MI355X_MICROARCH.md)
-constexpr int kSC1 = 16;
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-template <int AUX>
-__device__ __forceinline__ void bload8_aux(Raw8<f16>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff) {
-    r.x = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, AUX));
-}
-template <int AUX>
-__device__ __forceinline__ void bload8_aux(Raw8<float>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff) {
-    r.a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, AUX));
-    r.b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16, 0, AUX));
-}
-// One split's term of the split merge, O += w_s·Ô_s, L += w_s with w_s = l_s·2^(m_s - M):
-// shared by the combine kernel and the in-launch combine with contraction off, so both forms
-// round identically (bitwise-equal outputs whichever runs).
-__device__ __forceinline__ float split_weight(float2 ml, float M) {
-#pragma clang fp contract(off)
-    return (ml.x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml.x - M) * ml.y;
-}
-__device__ __forceinline__ void split_accumulate(f32x4& acc, float w, f32x4 v) {
-#pragma clang fp contract(off)
-    acc = acc + w * v;
-}
-// (an fp32 product, then the output rounding: never fused into one mixed-precision FMA)
-__device__ __forceinline__ f32x4 split_scale(f32x4 acc, float inv) {
-#pragma clang fp contract(off)
-    return acc * inv;
-}
-// 4-dim forms (workgroups with more threads than (row, 8-dim) items split rows into 16 chunks)
-template <typename T> struct Raw4;
-template <> struct Raw4<f16> { f16x4 x; };
-template <> struct Raw4<float> { f32x4 a; };
-template <int AUX>
-__device__ __forceinline__ void bload4_aux(Raw4<f16>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff) {
-    r.x = __builtin_bit_cast(f16x4, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, 0, AUX));
-}
-template <int AUX>
-__device__ __forceinline__ void bload4_aux(Raw4<float>& r, __amdgpu_buffer_rsrc_t rs, unsigned voff) {
-    r.a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, AUX));
-}
-__device__ __forceinline__ f32x4 raw4_to_f32(const Raw4<f16>& r) {
-    return f32x4{(float)r.x[0], (float)r.x[1], (float)r.x[2], (float)r.x[3]};
-}
-__device__ __forceinline__ f32x4 raw4_to_f32(const Raw4<float>& r) { return r.a; }
-template <typename T, int AUX>
-__device__ __forceinline__ void store4b(__amdgpu_buffer_rsrc_t rs, unsigned voff, f32x4 a) {
-    if constexpr (sizeof(T) == 2) {
-        const f16x4 h = f16x4{(f16)a[0], (f16)a[1], (f16)a[2], (f16)a[3]};
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, h), rs, voff, 0, AUX);
-    } else {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, a), rs, voff, 0, AUX);
-    }
-}
-// DPT dims of one row (DPT = 8: a0 = dims 0-3, a1 = 4-7; DPT = 4: a0 only)
-template <typename T, int DPT, int AUX>
-__device__ __forceinline__ void store_dims(__amdgpu_buffer_rsrc_t rs, unsigned voff, f32x4 a0, f32x4 a1) {
-    if constexpr (DPT == 8) store8<T, AUX>(rs, voff, a0, a1);
-    else store4b<T, AUX>(rs, voff, a0);
-}
-__device__ __forceinline__ void raw8_to_f32(const Raw8<f16>& r, f32x4& lo, f32x4& hi) {
-    lo = f32x4{(float)r.x[0], (float)r.x[1], (float)r.x[2], (float)r.x[3]};
-    hi = f32x4{(float)r.x[4], (float)r.x[5], (float)r.x[6], (float)r.x[7]};
-}
-__device__ __forceinline__ void raw8_to_f32(const Raw8<float>& r, f32x4& lo, f32x4& hi) {
-    lo = r.a;
-    hi = r.b;
-}
 
 // ----------------------------------------------------------------------------------------
 // Main kernel. Grid: x = query blocks of 32*QW rows, y = batch*heads, z = KV splits.
@@ -1261,9 +969,47 @@ size_t split_workspace_bytes(const Call& c, int splits) {
     return align256(o_bytes) + align256(rows * sizeof(float2));
 }
 
+static bool direct_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("MHA_HD64_DIRECT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// Tiles of 64 keys per wave of the single-pass kernel for this launch, or 0 if it does not apply:
+// fp16 input, every call's keys within 8 waves x 2 tiles, and at most 256 workgroups of 32 rows
+// (one residency round: the launches the ring kernel can only fill by splitting the keys).
+static int direct_tiles_for(const Call* calls, int n, InType in, bool forced) {
+    if (in != InType::F16 || (!forced && !direct_enabled())) return 0;
+    long wgs = 0;
+    int tiles = 1;
+    for (int i = 0; i < n; ++i) {
+        if (calls[i].nkv > 8 * 2 * kTileKV) return 0;
+        tiles = std::max(tiles, (calls[i].nkv + 8 * kTileKV - 1) / (8 * kTileKV));
+        wgs += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 31) / 32);
+    }
+    return (forced || wgs <= 256) ? tiles : 0;
+}
+
 GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_waves, int force_kv_waves,
-                     int force_splits) {
+                     int force_splits, InType in) {
     GroupPlan p{};
+    if (force_q_waves == kForceDirect || force_q_waves == 0) {
+        const int dt = direct_tiles_for(calls, n, in, force_q_waves == kForceDirect);
+        if (dt > 0) {
+            p.q_waves = 1;
+            p.kv_waves = 8;
+            p.rows_per_wave = 32;
+            p.direct_tiles = dt;
+            for (int i = 0; i < n; ++i) {
+                p.splits[i] = 1;
+                p.tiles_per_split[i] = 1;
+            }
+            return p;
+        }
+        if (force_q_waves == kForceDirect) force_q_waves = 0;  // not applicable: the planner's choice
+    }
     // Forced shapes (test/bench hook): q_waves >= 10 selects 64-row waves (RB = 2) of q_waves - 10.
     int rb = force_q_waves >= 10 ? 2 : 1;
     int qw = force_q_waves >= 10 ? force_q_waves - 10 : force_q_waves, kw = force_kv_waves;
@@ -1326,7 +1072,7 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
         }
         p.ws_needed = off;
         if (ok && off <= ws_bytes) return p;
-        return plan_group(calls, n, ws_bytes, 2, 2, force_splits);
+        return plan_group(calls, n, ws_bytes, 2, 2, force_splits, in);
     }
     for (;;) {
         size_t off = 0;
@@ -1345,8 +1091,9 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
     return p;
 }
 
-LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves, int force_kv_waves, int force_splits) {
-    const GroupPlan g = plan_group(&c, 1, ws_bytes, force_q_waves, force_kv_waves, force_splits);
+LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves, int force_kv_waves, int force_splits,
+                     InType in) {
+    const GroupPlan g = plan_group(&c, 1, ws_bytes, force_q_waves, force_kv_waves, force_splits, in);
     LaunchPlan p{};
     p.q_waves = g.q_waves;
     p.kv_waves = g.kv_waves;
@@ -1354,13 +1101,15 @@ LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves, int forc
     p.splits = g.splits[0];
     p.tiles_per_split = g.tiles_per_split[0];
     p.ws_needed = g.ws_needed;
+    p.direct_tiles = g.direct_tiles;
     return p;
 }
 
 static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutType out, void* workspace,
                                      size_t ws_bytes, hipStream_t stream, int force_q_waves, int force_kv_waves,
                                      int force_splits, int phase_mask) {
-    const GroupPlan p = plan_group(calls, n, workspace ? ws_bytes : 0, force_q_waves, force_kv_waves, force_splits);
+    const GroupPlan p =
+        plan_group(calls, n, workspace ? ws_bytes : 0, force_q_waves, force_kv_waves, force_splits, in);
     FwdArgs a{};
     CombineArgs cb{};
     a.stamps = g_stamps;
@@ -1402,6 +1151,11 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
     a.n_calls = n_live;
     a.total_blocks = blocks;
     const int rbw = p.rows_per_wave / 32;
+    if (p.direct_tiles > 0) {  // single-pass kernel: no split, no workspace
+        g_last_combine = 0;
+        if (!(phase_mask & 1)) return hipSuccess;
+        return launch_direct(a, blocks, p.direct_tiles, out == OutType::F32, stream);
+    }
     // Split calls combine inside the main launch when a ticket array is available (phase_mask 3,
     // the production form); otherwise (or MHA_HD64_FUSED_COMBINE=0) in the combine kernel.
     if (any_split && (phase_mask & 3) == 3 && fused_enabled()) a.tickets = tickets_for(stream, blocks);

@@ -211,16 +211,20 @@ def test_launch_rejects_misaligned_and_null(lib):
 def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
     out = (ctypes.c_int32 * 4)()
     # metric shape 1x4x1024x1024 inside the fixed 5,242,880 B workspace
+    # (single-pass kernel, plan code 21: 128 workgroups of 32 rows x all 1024 keys, no split,
+    # no workspace)
     need = lib.mha_hd64_plan(1, 4, 1024, 1024, 5242880, out)
     qw, kw, splits, tps = list(out)
-    wgs = (1024 // (32 * qw)) * 4 * splits
-    assert need <= 5242880 and wgs >= 128 and splits >= 2
-    assert (qw, kw, tps) == (1, 8, 1)  # one 512-key super-tile per split
+    assert need == 0 and (qw, kw, splits) == (21, 8, 1)
+    # past 1024 keys the ring kernel splits the keys within the fixed workspace
+    need = lib.mha_hd64_plan(1, 4, 1024, 2048, 5242880, out)
+    qw, kw, splits, tps = list(out)
+    assert need <= 5242880 and splits >= 2 and qw != 21
     # max length still fits
     need = lib.mha_hd64_plan(1, 4, 2048, 2048, 5242880, out)
     assert need <= 5242880
     # no workspace -> no split
-    lib.mha_hd64_plan(1, 4, 1024, 1024, 0, out)
+    lib.mha_hd64_plan(1, 4, 1024, 2048, 0, out)
     assert out[2] == 1
     # a big batch needs no split
     lib.mha_hd64_plan(64, 4, 1024, 1024, 1 << 30, out)

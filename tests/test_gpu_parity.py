@@ -239,7 +239,8 @@ def test_graph_capture_replay(dev):
         mha_hd64(q, k, v, out=out)
     from lightglue_amd import _lib
 
-    assert _lib.load().mha_hd64_last_combine_form() == 1  # one launch, splits merged in it
+    # one launch either way: the single-pass kernel (0, no split) or splits merged in-launch (1)
+    assert _lib.load().mha_hd64_last_combine_form() in (0, 1)
     out.zero_()
     g.replay()
     torch.cuda.synchronize()
@@ -442,14 +443,14 @@ def test_fused_combine_graphs_from_one_stream_replayed_concurrently(dev):
         q, k, v = (_t(x, dev, torch.float16) for x in (qn, kn, vn))
         ws = torch.empty(16 << 20, dtype=torch.uint8, device=dev)
         ref = torch.empty_like(q)
-        _forced(lib, q, k, v, ref, nq, nkv, 0, 0, 0, ws)
+        _forced(lib, q, k, v, ref, nq, nkv, 1, 8, 0, ws)  # the split plan (tickets)
         data.append((q, k, v, ref, torch.empty_like(q), ws, nq, nkv))
     torch.cuda.synchronize()
     graphs = []
     for q, k, v, _, out, ws, nq, nkv in data:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=cap):
-            _forced(lib, q, k, v, out, nq, nkv, 0, 0, 0, ws, stream=cap)
+            _forced(lib, q, k, v, out, nq, nkv, 1, 8, 0, ws, stream=cap)
         assert lib.mha_hd64_last_combine_form() == 1  # recorded with its own tickets
         graphs.append(g)
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
@@ -462,3 +463,112 @@ def test_fused_combine_graphs_from_one_stream_replayed_concurrently(dev):
         for d, s in zip(data, streams):
             torch.cuda.current_stream().wait_stream(s)
             assert torch.equal(d[4], d[3])
+
+
+# ---- single-pass kernel (csrc/mha_hd64_direct.hip; forced plan 21, the planner's choice for
+# fp16 launches of <= 256 32-row blocks with nkv <= 1024) ----
+DIRECT_SHAPES = [(1, 1), (33, 65), (100, 77), (256, 256), (1000, 777), (1024, 1024), (64, 1024), (513, 513),
+                 (2048, 1000), (300, 129), (97, 600), (5, 1024), (1024, 64), (130, 520)]
+
+
+@pytest.mark.parametrize("nq,nkv", DIRECT_SHAPES)
+def test_direct_kernel_matches_oracle(nq, nkv, dev, oracle_mod):
+    """Every key-tile layout: waves wholly past nkv, partial tiles, one- and two-tile waves."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    qn, kn, vn = synth.qkv(77 + nq + 3 * nkv, nq, nkv)
+    q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
+    rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 48)), nq - 1])
+    ref = oracle_mod.attention_c(np.ascontiguousarray(q16[:, :, rows]), k16, v16)
+    q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
+        o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
+        _forced(lib, q, k, v, o, nq, nkv, 21, 0, 0, ws)
+        assert lib.mha_hd64_last_combine_form() == 0
+        torch.cuda.synchronize()
+        got = o.float().cpu().numpy()
+        assert np.isfinite(got).all(), "unwritten or NaN output rows"
+        assert _maxdiff(got[:, :, rows], ref) <= tol
+
+
+def test_direct_kernel_rescale_and_masked_waves(dev, oracle_mod):
+    """A spike in a wave's second tile forces the rescale of the first tile's probabilities (key
+    100: wave 0, tile 1; key 1000: wave 7, tile 1); nkv = 600 leaves waves 5-7 without keys."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    nq = 256
+    for nkv, krow, gain in ((1024, 100, 6.0), (1024, 1000, 3.0), (600, 590, 6.0), (600, 10, 0.5)):
+        qn, kn, vn = synth.qkv(606 + nkv + krow, nq, nkv)
+        kn = synth.spike(qn, kn, 5, krow, gain)
+        q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
+        ref = oracle_mod.attention_c(q16, k16, v16)
+        q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+        o = torch.empty_like(q)
+        _forced(lib, q, k, v, o, nq, nkv, 21, 0, 0, ws)
+        torch.cuda.synchronize()
+        assert _maxdiff(o.float().cpu().numpy(), ref) <= TOL, (nkv, krow, gain)
+
+
+def test_direct_kernel_grouped_and_batched(dev, oracle_mod):
+    """The planner's single-pass launches: a LightGlue layer's pair of self calls at N=512 and
+    N=1024 (two calls, one launch) and a batched call, against the oracle; group of one is
+    bitwise the single launch."""
+    from lightglue_amd import _lib, mha_hd64_batched, mha_hd64_grouped
+
+    lib = _lib.load()
+    for n0, n1 in ((512, 512), (1024, 1024), (1000, 777)):
+        host = _group_inputs([(1, n0, n0), (1, n1, n1)], 41 + n0)
+        dev_t = [tuple(_t(x, dev, torch.float16) for x in c) for c in host]
+        outs = mha_hd64_grouped(dev_t)
+        assert lib.mha_hd64_last_combine_form() == 0
+        torch.cuda.synchronize()
+        for c, o in zip(host, outs):
+            assert _maxdiff(o.float().cpu().numpy(), oracle_mod.attention_c(*c)) <= TOL
+    (c,) = _group_inputs([(2, 300, 900)], 3)
+    q, k, v = (_t(x, dev, torch.float16) for x in c)
+    a = mha_hd64_batched(q, k, v)
+    (b,) = mha_hd64_grouped([(q, k, v)])
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert _maxdiff(a.float().cpu().numpy(), oracle_mod.attention_c(*c)) <= TOL
+
+
+def test_direct_kernel_forced_outside_its_range_is_rejected(dev):
+    from lightglue_amd import _lib
+
+    lib = _lib.load()
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    for nkv, dt in ((1025, torch.float16), (512, torch.float32)):
+        q = torch.zeros(1, 4, 64, 64, dtype=dt, device=dev)
+        k = torch.zeros(1, 4, nkv, 64, dtype=dt, device=dev)
+        o = torch.empty_like(q)
+        st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), k.data_ptr(), o.data_ptr(), 1, 4, 64, nkv,
+                                        int(dt == torch.float32), int(dt == torch.float32), 21, 0, 0,
+                                        ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream, 3)
+        assert st == 1, (nkv, dt)
+
+
+def test_direct_kernel_deterministic_and_capturable(dev):
+    from lightglue_amd import mha_hd64, synth
+
+    qn, kn, vn = synth.qkv(12, 1024, 1024)
+    q, k, v = (_t(x, dev, torch.float16) for x in (qn, kn, vn))
+    a = mha_hd64(q, k, v).clone()
+    b = mha_hd64(q, k, v).clone()
+    out = torch.empty_like(q)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        mha_hd64(q, k, v, out=out)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        mha_hd64(q, k, v, out=out)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(out, a)

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build a library variant of the single-pass kernel (A/B experiments; never shipped):
+#   tools/build_direct_variant.sh <name> [extra hipcc flags...]  -> lib/exp/libmha_hd64_<name>.so
+# (run with MHA_HD64_LIB=lib/exp/libmha_hd64_<name>.so)
+set -e
+NAME=$1; shift
+cd "$(dirname "$0")/../lightglue-with-flashattentionv2-tensorrt_amd"
+mkdir -p lib/exp
+make -s lib/libmha_hd64.so
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans "$@" \
+      -I../include -Icsrc -c csrc/mha_hd64_direct.hip -o lib/exp/d_$NAME.o
+hipcc --offload-arch=gfx950 -shared -fPIC lib/obj/mha_hd64_kernels.o lib/exp/d_$NAME.o lib/obj/mha_hd64_plugin.o \
+      lib/obj/lightglue_glue.o -o lib/exp/libmha_hd64_$NAME.so
+rm -f lib/exp/d_$NAME.o
+echo lib/exp/libmha_hd64_$NAME.so
