@@ -28,11 +28,28 @@
 #include "mha_hd64_device.h"
 #include "mha_hd64_internal.h"
 
+// Diagnostic timestamps (-DMHA_STAMPS builds, tools/dstamps.py): wave 0's s_memtime at phase
+// boundaries, without draining memory (the waits of the phase boundaries themselves are kept).
+#ifdef MHA_STAMPS
+#define DSTAMP(slot)                                                                              \
+    do {                                                                                          \
+        unsigned long long t_;                                                                    \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+        if (threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (slot)] = t_;                             \
+    } while (0)
+#else
+#define DSTAMP(slot) \
+    do {             \
+    } while (0)
+#endif
+
+
 namespace mha_hd64 {
 namespace {
 
 template <typename TOut, int TPW, bool MULTI>
 __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
+    // (16 waves x 1 tile, four per SIMD, measured 7.7 us against 6.3 us for 8 x 2 at 1x4x1024x1024)
     constexpr int KW = 8;                               // waves (key slices) per workgroup
     constexpr int BLOCK_M = 32;                         // query rows per workgroup
     constexpr int WAVE_KEYS = kTileKV * TPW;            // keys per wave
@@ -46,6 +63,7 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     lds_char* const lds = (lds_char*)smem;
 
+    DSTAMP(0);
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
@@ -89,17 +107,9 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
 
     if (n_t > 0) {
         // ---- loads, all up front (unconditional: rows past nkv read as zero) ----
-        Raw8<f16> qraw[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            if (MHA_ABL & ABL_NO_GLOAD) qraw[s].x = f16x8{} + (f16)(lane * 0.01f);
-            else bload8(qraw[s], q_rs, (unsigned)(q_row * kHeadDim + 16 * s + 8 * hh) * 2, 0);
-        }
-        // K, then V, of this wave's TPW tiles reach LDS by LDS-DMA in whole 128-B rows (1 KiB per
-        // instruction: rows 8i..8i+7), swizzled on the source side (the DMA writes lane-linear):
-        // LDS position p of row `row` receives the 16-B chunk p ^ swz(row) (k_off / v_off images).
-        // K and V take turns in the wave's region: K's fragments are read into registers, then
-        // V lands over them while QKᵀ and the softmax run.
+        // K reaches LDS by LDS-DMA in whole 128-B rows (1 KiB per instruction: rows 8i..8i+7),
+        // swizzled on the source side (the DMA writes lane-linear): LDS position p of row `row`
+        // receives the 16-B chunk p ^ swz(row) (the k_off / v_off images).
         auto dma_rows = [&](__amdgpu_buffer_rsrc_t rs, bool is_k) {
 #pragma unroll
             for (int i = 0; i < 8 * TPW; ++i) {
@@ -111,30 +121,49 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
                     (unsigned)((key0 + row) * kHeadDim + ch * 8) * 2, 0, 0, 0);
             }
         };
-        dma_rows(k_rs, true);
-        // (the compiler does not order these LDS reads after the DMA: wait for it explicitly)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        // K fragments (A operand of Sᵀ = K·Qᵀ): kf[t][2s] = K[64t+r][16s+8hh..+7], kf[t][2s+1] = rows +32
-        f16x8 kf[TPW][8];
+        auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, int t) {  // V of tile t into slot t
 #pragma unroll
-        for (int t = 0; t < TPW; ++t)
+            for (int i = 8 * t; i < 8 * t + 8; ++i) {
+                const int row = 8 * i + (lane >> 3), pos = lane & 7;
+                const int ch = pos ^ (((row >> 1) & 1) << 2);
+                if (MHA_ABL & ABL_NO_GLOAD) continue;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * i), 16,
+                    (unsigned)((key0 + row) * kHeadDim + ch * 8) * 2, 0, 0, 0);
+            }
+        };
+        // K fragments of tile t (A operand of Sᵀ = K·Qᵀ): kf[2s] = K[64t+r][16s+8hh..+7], kf[2s+1] = rows +32
+        auto read_k = [&](int t, f16x8(&kf)[8]) {
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
                 for (int h2 = 0; h2 < 2; ++h2)
-                    kf[t][2 * s + h2] = lds_read16(lds, region + k_off(kTileKV * t + 32 * h2 + r, 2 * s + hh));
-        // Q fragments (B operand of Sᵀ = K·Qᵀ), scaled by 0.125·log2(e) in fp16.
-        f16x8 qf[4];
+                    kf[2 * s + h2] = lds_read16(lds, region + k_off(kTileKV * t + 32 * h2 + r, 2 * s + hh));
+        };
+        f16x8 qf[4];  // Q fragments (B operand of Sᵀ = K·Qᵀ), scaled by 0.125·log2(e) in fp16
+        // Q by plain loads in inline asm (unseen by the compiler's wait bookkeeping: a plain load's
+        // use behind an LDS-DMA would make it drain every DMA), K then V by DMA, tile by tile
+        // through the wave's two 8 KiB slots: tile t's V is issued into slot t as soon as K(t)'s
+        // fragments are in registers, so K(1) lands under QKᵀ(0) and V under all of the scores.
+        f16x8 qraw[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if (MHA_ABL & ABL_NO_GLOAD) qraw[s] = f16x8{} + (f16)(lane * 0.01f);
+            else asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen"
+                              : "=v"(qraw[s])
+                              : "v"((unsigned)(q_row * kHeadDim + 16 * s + 8 * hh) * 2), "s"(q_rs));
+        }
+        dma_rows(k_rs, true);
+        // Q and K(0) have landed (issue order: Q, K(0) 8 pieces, K(1) 8 pieces)
+        if constexpr (TPW == 2)
+            asm volatile("s_waitcnt vmcnt(8)" : "+v"(qraw[0]), "+v"(qraw[1]), "+v"(qraw[2]), "+v"(qraw[3])::"memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(qraw[0]), "+v"(qraw[1]), "+v"(qraw[2]), "+v"(qraw[3])::"memory");
+        DSTAMP(1);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) qf[s][e] = (f16)((float)qraw[s].x[e] * kScaleLog2);
-
-        // every K fragment is in registers before V's DMA overwrites the region; Q is consumed
-        // (scaled) before it too, so no Q use waits behind the V DMA (the compiler drains all
-        // outstanding loads at a plain load's use while an LDS-DMA is in flight)
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3])::"memory");
-        dma_rows(v_rs, false);
+            for (int e = 0; e < 8; ++e) qf[s][e] = (f16)((float)qraw[s][e] * kScaleLog2);
 
         // Row sums on the matrix pipe and the bias k-step: as the ring kernel (mha_hd64_kernels.hip).
         const f16 sel = (((lane & 15) >> 2) & 1) == ((lane >> 4) & 1) ? (f16)1.f : (f16)0.f;
@@ -162,6 +191,13 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
         f16x8 p[TPW][2][2];  // P (fp16) as the B operand: p[t][half][k-step]
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
+            f16x8 kf[8];
+            if (t > 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K(t) landed; V(t-1) may not have
+            read_k(t, kf);
+            // K(t)'s fragments are in registers before V(t)'s DMA overwrites slot t
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]), "+v"(kf[4]),
+                         "+v"(kf[5]), "+v"(kf[6]), "+v"(kf[7])::"memory");
+            dma_tile(v_rs, t);
             // Sᵀ = K·Qᵀ - m (bias k-step first), two 32-key halves
             const bool partial = key0 + kTileKV * (t + 1) > nkv;
             const f16x8 ab0 = partial ? a_bias_of(t, 0) : f16x8{one_h, one_h, 0, 0, 0, 0, 0, 0};
@@ -172,12 +208,12 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 if (MHA_ABL & ABL_NO_QK) {
-                    keep_live(kf[t][2 * s]);
-                    keep_live(kf[t][2 * s + 1]);
+                    keep_live(kf[2 * s]);
+                    keep_live(kf[2 * s + 1]);
                     continue;
                 }
-                c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][2 * s], qf[s], c0, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[t][2 * s + 1], qf[s], c1, 0, 0, 0);
+                c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s], qf[s], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s + 1], qf[s], c1, 0, 0, 0);
             }
             const float mx = xhalf_max(tree_max(c0, c1));
             // online softmax: the first tile sets the max; a later one moves it only when a query's
@@ -213,10 +249,14 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
                 p[t][1][1][e] = (f16)c1[8 + e];
             }
         }
-        // Phase 2: V has landed (DMA) -> Oᵀ = Vᵀ·Pᵀ and the row sums.
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        DSTAMP(2);
+        // Phase 2: V in LDS -> Oᵀ = Vᵀ·Pᵀ and the row sums.
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
+            // V(t) landed (V(t+1)'s 8 pieces may still be in flight)
+            if (t + 1 < TPW) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (t == 0) DSTAMP(3);
             const unsigned va0 = region + t * kTileBytes + v_lane + 64 * vb;
             const unsigned va1 = region + t * kTileBytes + v_lane + 64 * (1 - vb);
 #pragma unroll
@@ -239,6 +279,7 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
         }
     }
 
+    DSTAMP(4);
     // ---- epilogue: merge the 8 key slices through LDS ----
     // The wave's V region is its own, so its staged Oᵀ overwrites only what it has read itself.
     float* ol = reinterpret_cast<float*>(smem + region);      // [32][OROW]
@@ -257,6 +298,7 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
         if (hh == 0) *reinterpret_cast<float2*>(mlb + (wave * BLOCK_M + r) * 2) = make_float2(m_w, L_w);
     }
     __syncthreads();
+    DSTAMP(5);
     // thread -> (row, 4 dims): 32 rows x 16 chunks = 512 items
     const int row = tid >> 4, c = (tid & 15) * 4;
     const int q = qtile * BLOCK_M + row;
@@ -280,6 +322,10 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
                                                       (unsigned)(nq * kHeadDim * sizeof(TOut)));
         store4b<TOut, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)), acc * (1.f / L));
     }
+#ifdef MHA_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    DSTAMP(6);
+#endif
 }
 
 template <typename TOut, int TPW>
