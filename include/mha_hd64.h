@@ -135,7 +135,9 @@ size_t mha_hd64_get_workspace_size(const mha_hd64_plugin_t* p,
  *   HALF  -> fp16 in, fp32 accumulation, fp16 out   (reference: pad -> fp16in_fp16out kernel -> unpad)
  *   FLOAT -> fp32 in rounded to fp16 (RN) on load, fp32 accumulation, fp32 out
  *            (reference: convert+pad -> fp16in_fp32out kernel -> unpad)
- * One kernel launch on `stream`. A call whose keys are split across workgroups merges the
+ * One kernel launch on `stream`. At the reference's shapes with N <= 1024 (HALF) a workgroup
+ * holds all keys of its 32 query rows (single-pass kernel, no split, no workspace use). A call
+ * whose keys are split across workgroups merges the
  * splits inside that launch through library-owned arrival tickets; the first enqueue on a
  * (device, stream) outside stream capture allocates them (and, once per device, a pre-zeroed
  * arena for captured launches, with one stream sync). Without tickets (first use of a stream

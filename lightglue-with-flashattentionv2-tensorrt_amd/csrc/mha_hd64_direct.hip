@@ -25,6 +25,8 @@
 // at most 256 such workgroups (one residency round); everything else runs the ring kernel.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "mha_hd64_device.h"
 #include "mha_hd64_internal.h"
 
@@ -101,36 +103,36 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
     const int n_t = max(0, min(TPW, (nkv - key0 + kTileKV - 1) / kTileKV));
     const unsigned region = (unsigned)wave * RS;
 
-    f32x16 o0 = {}, o1 = {};  // Oᵀ: dims 0..31 / 32..63, query on the lane
-    f32x4 l_acc = {0.f, 0.f, 0.f, 0.f};
+    f32x16 o0, o1;  // Oᵀ: dims 0..31 / 32..63, query on the lane
+    f32x4 l_acc;
     float m_run = 0.f;
 
-    if (n_t > 0) {
+    if (n_t == 0) {  // a wave wholly past nkv contributes nothing (m = -inf in the merge)
+        o0 = o1 = f32x16{};
+        l_acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
         // ---- loads, all up front (unconditional: rows past nkv read as zero) ----
         // K reaches LDS by LDS-DMA in whole 128-B rows (1 KiB per instruction: rows 8i..8i+7),
         // swizzled on the source side (the DMA writes lane-linear): LDS position p of row `row`
         // receives the 16-B chunk p ^ swz(row) (the k_off / v_off images).
-        auto dma_rows = [&](__amdgpu_buffer_rsrc_t rs, bool is_k) {
+        // Per-lane byte offsets: row 8i + lane/8 of the wave's slice, chunk swizzled; piece i adds
+        // i KiB (a scalar offset), and the swizzles repeat every two pieces (K) or never vary (V).
+        const unsigned lrow = (unsigned)(key0 + (lane >> 3)) * kHeadDim * 2;
+        const unsigned k_lane[2] = {lrow + (((lane & 7) ^ ((lane >> 4) & 7)) << 4),
+                                    lrow + (((lane & 7) ^ ((4 + (lane >> 4)) & 7)) << 4)};
+        const unsigned v_lane_off = lrow + (((lane & 7) ^ (((lane >> 4) & 1) << 2)) << 4);
+        auto dma_piece = [&](__amdgpu_buffer_rsrc_t rs, unsigned voff, int i) {
+            if (MHA_ABL & ABL_NO_GLOAD) return;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * i),
+                                                     16, voff, 1024 * i, 0, 0);
+        };
+        auto dma_rows = [&](__amdgpu_buffer_rsrc_t rs, bool is_k) {  // all of the wave's K
 #pragma unroll
-            for (int i = 0; i < 8 * TPW; ++i) {
-                const int row = 8 * i + (lane >> 3), pos = lane & 7;
-                const int ch = is_k ? (pos ^ ((row >> 1) & 7)) : (pos ^ (((row >> 1) & 1) << 2));
-                if (MHA_ABL & ABL_NO_GLOAD) continue;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * i), 16,
-                    (unsigned)((key0 + row) * kHeadDim + ch * 8) * 2, 0, 0, 0);
-            }
+            for (int i = 0; i < 8 * TPW; ++i) dma_piece(rs, is_k ? k_lane[i & 1] : v_lane_off, i);
         };
         auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, int t) {  // V of tile t into slot t
 #pragma unroll
-            for (int i = 8 * t; i < 8 * t + 8; ++i) {
-                const int row = 8 * i + (lane >> 3), pos = lane & 7;
-                const int ch = pos ^ (((row >> 1) & 1) << 2);
-                if (MHA_ABL & ABL_NO_GLOAD) continue;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * i), 16,
-                    (unsigned)((key0 + row) * kHeadDim + ch * 8) * 2, 0, 0, 0);
-            }
+            for (int i = 8 * t; i < 8 * t + 8; ++i) dma_piece(rs, v_lane_off, i);
         };
         // K fragments of tile t (A operand of Sᵀ = K·Qᵀ): kf[2s] = K[64t+r][16s+8hh..+7], kf[2s+1] = rows +32
         auto read_k = [&](int t, f16x8(&kf)[8]) {
@@ -198,23 +200,38 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]), "+v"(kf[4]),
                          "+v"(kf[5]), "+v"(kf[6]), "+v"(kf[7])::"memory");
             dma_tile(v_rs, t);
-            // Sᵀ = K·Qᵀ - m (bias k-step first), two 32-key halves
+            // Sᵀ = K·Qᵀ - m, two 32-key halves. The bias k-step (-m and the tail mask) runs first,
+            // except on a full first tile: there it runs last, once the tile's max is known, so the
+            // scores need no subtraction (an MFMA instead of 32 VALU ops).
             const bool partial = key0 + kTileKV * (t + 1) > nkv;
-            const f16x8 ab0 = partial ? a_bias_of(t, 0) : f16x8{one_h, one_h, 0, 0, 0, 0, 0, 0};
-            const f16x8 ab1 = partial ? a_bias_of(t, 1) : f16x8{one_h, one_h, 0, 0, 0, 0, 0, 0};
+            const bool bias_last = t == 0 && !partial;  // wave-uniform
+            const f16x8 a_plain = f16x8{one_h, one_h, 0, 0, 0, 0, 0, 0};
+            const f16x8 ab0 = partial ? a_bias_of(t, 0) : a_plain;
+            const f16x8 ab1 = partial ? a_bias_of(t, 1) : a_plain;
             const f32x16 zero = {};
-            f32x16 c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab0, b_bias, zero, 0, 0, 0);
-            f32x16 c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab1, b_bias, zero, 0, 0, 0);
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                if (MHA_ABL & ABL_NO_QK) {
-                    keep_live(kf[2 * s]);
-                    keep_live(kf[2 * s + 1]);
-                    continue;
+            f32x16 c0, c1;
+            // (two straight-line chains: each starts its accumulators from an inline 0)
+            auto chain = [&](auto bias_first_c) {
+                constexpr bool BF = decltype(bias_first_c)::value;
+                if constexpr (BF) {
+                    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab0, b_bias, zero, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab1, b_bias, zero, 0, 0, 0);
                 }
-                c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s], qf[s], c0, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s + 1], qf[s], c1, 0, 0, 0);
-            }
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    if (MHA_ABL & ABL_NO_QK) {
+                        keep_live(kf[2 * s]);
+                        keep_live(kf[2 * s + 1]);
+                        if (!BF && s == 0) c0 = c1 = zero;
+                        continue;
+                    }
+                    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s], qf[s], (!BF && s == 0) ? zero : c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s + 1], qf[s], (!BF && s == 0) ? zero : c1, 0, 0,
+                                                                0);
+                }
+            };
+            if (bias_last) chain(std::false_type{});
+            else chain(std::true_type{});
             const float mx = xhalf_max(tree_max(c0, c1));
             // online softmax: the first tile sets the max; a later one moves it only when a query's
             // tile max exceeds it by > kRescaleThr (wave-uniform branch). No PV has run yet, so a
@@ -231,9 +248,14 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
                             for (int ss = 0; ss < 2; ++ss) p[t2][h2][ss] *= alpha;
                 }
                 m_run += d;
-                c0 -= d;
-                c1 -= d;
                 set_bias();
+                if (bias_last) {
+                    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_plain, b_bias, c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a_plain, b_bias, c1, 0, 0, 0);
+                } else {
+                    c0 -= d;
+                    c1 -= d;
+                }
             }
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
@@ -272,9 +294,11 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
                         keep_live(p[t][jj][ss]);
                         continue;
                     }
-                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa, p[t][jj][ss], o0, 0, 0, 0);
-                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb, p[t][jj][ss], o1, 0, 0, 0);
-                    l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, p[t][jj][ss], l_acc, 0, 0, 0);
+                    const bool first = t == 0 && jj == 0 && ss == 0;  // accumulators start at inline 0
+                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa, p[t][jj][ss], first ? f32x16{} : o0, 0, 0, 0);
+                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb, p[t][jj][ss], first ? f32x16{} : o1, 0, 0, 0);
+                    l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, p[t][jj][ss], first ? f32x4{} : l_acc, 0,
+                                                                   0, 0);
                 }
         }
     }

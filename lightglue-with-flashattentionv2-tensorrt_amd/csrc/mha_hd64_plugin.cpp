@@ -355,7 +355,9 @@ const char* mha_hd64_last_error(void) { return g_last_error.c_str(); }
 void mha_hd64_set_abort_on_error(int32_t enable) { g_abort_on_error = enable != 0; }
 const char* mha_hd64_build_info(void) {
     return "mha_hd64: gfx950 (CDNA4) HIP kernels, v_mfma_f32_32x32x16_f16 + ds_read_b64_tr_b16; "
-           "variants fp16->fp16, fp16->fp32, fp32->fp32; workgroups (q,kv waves) 4x1 2x2 1x2 4x2 2x4, 2x2 with 64-row waves; software-pipelined QK(t+1)|softmax(t); split-KV combine";
+           "variants fp16->fp16, fp16->fp32, fp32->fp32; single-pass kernel (32 rows x all keys per workgroup, K/V by LDS-DMA) "
+           "for launches of <= 256 blocks with nkv <= 1024; LDS-ring kernel with workgroups (q,kv waves) 4x1 2x2 1x2 4x2 2x4 1x4 1x8, "
+           "2x2 with 64-row waves; software-pipelined QK(t+1)|softmax(t); split-KV combine (in-launch or kernel)";
 }
 
 // Test/bench hook (not part of include/mha_hd64.h): launch with a forced plan

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 recipe for the MHAHeadDim64 kernels (run on the GPU box from the repo root):
-#   bash profiles/pmc_passes.sh <workload: call|batched> <tag>
+#   bash tools/pmc_passes.sh <workload: call|batched> <tag>
 # Counter passes are separate runs (gfx950 slot limits; no --pmc beside trace domains).
 set -e
 W=${1:-batched}

@@ -1,6 +1,6 @@
-"""Summarise a profiles/pmc_passes.sh output directory for the main attention kernel.
+"""Summarise a tools/pmc_passes.sh output directory for the main attention kernel.
 
-    python profiles/summarize_pmc.py gpurun_out/prof_<tag>_<workload> [kernel-substring]
+    python tools/summarize_pmc.py gpurun_out/prof_<tag>_<workload> [kernel-substring]
 Prints per-dispatch means of every counter, the derived ratios used in DESIGN.md, and the
 HBM bytes per launch with the gfx950 FETCH_SIZE correction (x2, MI355X_MICROARCH.md §HBM)."""
 import collections
