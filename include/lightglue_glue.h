@@ -32,10 +32,22 @@ int32_t lg_qkv_rotary_split(int32_t dtype, const void* qkv, const void* cos, con
 int32_t lg_split_heads2(int32_t dtype, const void* a, const void* b, int32_t heads, int32_t n0, int32_t n1,
                         void* a0, void* a1, void* b0, void* b1, hipStream_t stream);
 
+/* The same with row stride `ld` elements for a and b (column views of one wider projection, e.g.
+ * the cross block's to_qk | to_v computed as one GEMM: a = qkv, b = qkv + heads*64, ld = 2*heads*64);
+ * a and b 16-byte aligned. */
+int32_t lg_split_heads2_ld(int32_t dtype, const void* a, const void* b, int32_t ld, int32_t heads, int32_t n0,
+                           int32_t n1, void* a0, void* a1, void* b0, void* b1, hipStream_t stream);
+
 /* Attention outputs back to rows (lightglue.py:118-120, 163-170): x0 [heads, n0, 64],
  * x1 [heads, n1, 64] -> out [n0+n1, heads*64]. */
 int32_t lg_merge_heads(int32_t dtype, const void* x0, const void* x1, int32_t heads, int32_t n0, int32_t n1,
                        void* out, hipStream_t stream);
+
+/* The FFN input of both blocks (lightglue.py:104, 181: cat([x, message], -1)) with the message
+ * projection folded into the FFN's first weight: out [n0+n1, 2*heads*64] = [x | merge(x0, x1)],
+ * x [n0+n1, heads*64]. One pass instead of merge_heads + a concatenation copy. */
+int32_t lg_merge_heads_cat(int32_t dtype, const void* x, const void* x0, const void* x1, int32_t heads, int32_t n0,
+                           int32_t n1, void* out, hipStream_t stream);
 
 /* FFN middle (lightglue.py:101-106): y = GELU(LayerNorm(x) * gamma + beta), exact (erf) GELU,
  * x, y [rows, dim], dim a multiple of 64 and <= 1024. */

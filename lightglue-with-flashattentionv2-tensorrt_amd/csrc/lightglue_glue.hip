@@ -58,7 +58,7 @@ template <> struct V16<float> { typedef unsigned int type __attribute__((ext_vec
 // ---- [rows, heads*64] <-> per image [heads, ni, 64] (thread = one 16-B chunk) ----
 template <typename T, bool SPLIT>
 __global__ __launch_bounds__(256) void heads_kernel(const T* a, const T* b, T* a0, T* a1, T* b0, T* b1, int heads,
-                                                    int n0, int n1) {
+                                                    int n0, int n1, int ld) {
     typedef typename V16<T>::type vec;
     constexpr int E = V16<T>::n;
     constexpr int CH = kD / E;  // chunks per head row
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void heads_kernel(const T* a, const T* b, T* a
     const int n = i / ((long)CH * heads);
     const bool first = n < n0;
     const int row = first ? n : n - n0, nn = first ? n0 : n1;
-    const size_t rows_off = (size_t)n * heads * kD + h * kD + c * E;
+    const size_t rows_off = (size_t)n * ld + h * kD + c * E;  // row-major side: row stride ld
     const size_t head_off = ((size_t)h * nn + row) * kD + c * E;
     if (SPLIT) {
         const T* src = second ? b : a;
@@ -83,6 +83,33 @@ __global__ __launch_bounds__(256) void heads_kernel(const T* a, const T* b, T* a
         const T* src = first ? a : b;
         *reinterpret_cast<vec*>(a0 + rows_off) = *reinterpret_cast<const vec*>(src + head_off);
     }
+}
+
+// [x | merge_heads(x0, x1)]: one 16-B chunk of a 2*heads*64-wide output row per thread; the left
+// half copies x (the FFN's concatenation, lightglue.py:104/181), the right half gathers the
+// head-major attention outputs.
+template <typename T>
+__global__ __launch_bounds__(256) void merge_cat_kernel(const T* x, const T* x0, const T* x1, T* out, int heads,
+                                                        int n0, int n1) {
+    typedef typename V16<T>::type vec;
+    constexpr int E = V16<T>::n;
+    constexpr int CH = kD / E;
+    const int ntot = n0 + n1;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int half = CH * heads;  // chunks per half row
+    if (idx >= (long)ntot * 2 * half) return;
+    const int cc = idx % (2 * half);
+    const int n = idx / (2 * half);
+    vec v;
+    if (cc < half) {
+        v = *reinterpret_cast<const vec*>(x + (size_t)n * heads * kD + cc * E);
+    } else {
+        const int c2 = cc - half, h = c2 / CH, c = c2 % CH;
+        const bool first = n < n0;
+        const int row = first ? n : n - n0, nn = first ? n0 : n1;
+        v = *reinterpret_cast<const vec*>((first ? x0 : x1) + ((size_t)h * nn + row) * kD + c * E);
+    }
+    *reinterpret_cast<vec*>(out + (size_t)n * 2 * heads * kD + cc * E) = v;
 }
 
 __device__ __forceinline__ float wave_sum(float x) {
@@ -210,18 +237,25 @@ int32_t lg_qkv_rotary_split(int32_t dtype, const void* qkv, const void* cosv, co
 
 int32_t lg_split_heads2(int32_t dtype, const void* a, const void* b, int32_t heads, int32_t n0, int32_t n1,
                         void* a0, void* a1, void* b0, void* b1, hipStream_t stream) {
-    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || !a)
-        return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_split_heads2", "bad arguments");
+    return lg_split_heads2_ld(dtype, a, b, heads * kD, heads, n0, n1, a0, a1, b0, b1, stream);
+}
+
+int32_t lg_split_heads2_ld(int32_t dtype, const void* a, const void* b, int32_t ld, int32_t heads, int32_t n0,
+                           int32_t n1, void* a0, void* a1, void* b0, void* b1, hipStream_t stream) {
     const int E = dtype == MHA_HD64_DT_HALF ? 8 : 4;
+    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || !a || ld < heads * kD || ld % E != 0 ||
+        (reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) % 16 != 0)
+        return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_split_heads2", "bad arguments");
+    
     const long threads = (b ? 2 : 1) * (long)(n0 + n1) * heads * (kD / E);
     if (threads == 0) return MHA_HD64_STATUS_SUCCESS;
     if (dtype == MHA_HD64_DT_HALF)
         hipLaunchKernelGGL((heads_kernel<f16, true>), dim3(blocks_for(threads)), dim3(256), 0, stream, (const f16*)a,
-                           (const f16*)b, (f16*)a0, (f16*)a1, (f16*)b0, (f16*)b1, heads, n0, n1);
+                           (const f16*)b, (f16*)a0, (f16*)a1, (f16*)b0, (f16*)b1, heads, n0, n1, ld);
     else
         hipLaunchKernelGGL((heads_kernel<float, true>), dim3(blocks_for(threads)), dim3(256), 0, stream,
                            (const float*)a, (const float*)b, (float*)a0, (float*)a1, (float*)b0, (float*)b1, heads,
-                           n0, n1);
+                           n0, n1, ld);
     return launched("lg_split_heads2");
 }
 
@@ -234,12 +268,29 @@ int32_t lg_merge_heads(int32_t dtype, const void* x0, const void* x1, int32_t he
     if (threads == 0) return MHA_HD64_STATUS_SUCCESS;
     if (dtype == MHA_HD64_DT_HALF)
         hipLaunchKernelGGL((heads_kernel<f16, false>), dim3(blocks_for(threads)), dim3(256), 0, stream,
-                           (const f16*)x0, (const f16*)x1, (f16*)out, nullptr, nullptr, nullptr, heads, n0, n1);
+                           (const f16*)x0, (const f16*)x1, (f16*)out, nullptr, nullptr, nullptr, heads, n0, n1,
+                           heads * kD);
     else
         hipLaunchKernelGGL((heads_kernel<float, false>), dim3(blocks_for(threads)), dim3(256), 0, stream,
                            (const float*)x0, (const float*)x1, (float*)out, nullptr, nullptr, nullptr, heads, n0,
-                           n1);
+                           n1, heads * kD);
     return launched("lg_merge_heads");
+}
+
+int32_t lg_merge_heads_cat(int32_t dtype, const void* x, const void* x0, const void* x1, int32_t heads, int32_t n0,
+                           int32_t n1, void* out, hipStream_t stream) {
+    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || !x || !out)
+        return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_merge_heads_cat", "bad arguments");
+    const int E = dtype == MHA_HD64_DT_HALF ? 8 : 4;
+    const long threads = (long)(n0 + n1) * 2 * heads * (kD / E);
+    if (threads == 0) return MHA_HD64_STATUS_SUCCESS;
+    if (dtype == MHA_HD64_DT_HALF)
+        hipLaunchKernelGGL((merge_cat_kernel<f16>), dim3(blocks_for(threads)), dim3(256), 0, stream, (const f16*)x,
+                           (const f16*)x0, (const f16*)x1, (f16*)out, heads, n0, n1);
+    else
+        hipLaunchKernelGGL((merge_cat_kernel<float>), dim3(blocks_for(threads)), dim3(256), 0, stream,
+                           (const float*)x, (const float*)x0, (const float*)x1, (float*)out, heads, n0, n1);
+    return launched("lg_merge_heads_cat");
 }
 
 int32_t lg_layernorm_gelu(int32_t dtype, const void* x, const void* gamma, const void* beta, int32_t rows,

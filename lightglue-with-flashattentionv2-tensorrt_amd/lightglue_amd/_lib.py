@@ -125,6 +125,8 @@ SIGNATURES.update({
     "lg_qkv_rotary_split": ([_I, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P], _I),
     "lg_split_heads2": ([_I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P], _I),
     "lg_merge_heads": ([_I, _P, _P, _I, _I, _I, _P, _P], _I),
+    "lg_split_heads2_ld": ([_I, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P], _I),
+    "lg_merge_heads_cat": ([_I, _P, _P, _P, _I, _I, _I, _P, _P], _I),
     "lg_layernorm_gelu": ([_I, _P, _P, _P, _I, _I, ctypes.c_float, _P, _P], _I),
     "lg_log_double_softmax_workspace": ([_I, _I], _S),
     "lg_log_double_softmax": ([_P, _P, _P, _I, _I, _P, _P, _P], _I),

@@ -71,6 +71,29 @@ class _Hip:
         return (a0, a1), (b0, b1)
 
     @staticmethod
+    def split_heads2_ld(ab, heads, splits):
+        """ab [1, N0+N1, 2*heads*64] = [a | b] (one GEMM's output) -> per image (a_i, b_i) heads."""
+        n0, n1 = splits
+        mk = lambda n: torch.empty((1, heads, n, 64), dtype=ab.dtype, device=ab.device)  # noqa: E731
+        a0, a1, b0, b1 = mk(n0), mk(n1), mk(n0), mk(n1)
+        half = heads * 64
+        st = _lib.load().lg_split_heads2_ld(_DT[ab.dtype], ab.data_ptr(), ab.data_ptr() + half * ab.element_size(),
+                                            2 * half, heads, n0, n1, a0.data_ptr(), a1.data_ptr(), b0.data_ptr(),
+                                            b1.data_ptr(), _Hip._stream(ab))
+        _check(st, "lg_split_heads2_ld")
+        return (a0, a1), (b0, b1)
+
+    @staticmethod
+    def merge_heads_cat(x, x0, x1):
+        """[x | merge_heads(x0, x1)] -> [1, N0+N1, 2*heads*64] (the FFN input)."""
+        heads, n0, n1 = x0.shape[1], x0.shape[2], x1.shape[2]
+        out = torch.empty((1, n0 + n1, 2 * heads * 64), dtype=x.dtype, device=x.device)
+        st = _lib.load().lg_merge_heads_cat(_DT[x.dtype], x.data_ptr(), x0.data_ptr(), x1.data_ptr(), heads, n0, n1,
+                                            out.data_ptr(), _Hip._stream(x))
+        _check(st, "lg_merge_heads_cat")
+        return out
+
+    @staticmethod
     def merge_heads(x0, x1):
         heads, n0, n1 = x0.shape[1], x0.shape[2], x1.shape[2]
         out = torch.empty((1, n0 + n1, heads * 64), dtype=x0.dtype, device=x0.device)
@@ -99,6 +122,39 @@ class _Hip:
                                        ws.data_ptr(), stream)
         _check(st, "lg_log_double_softmax")
         return out
+
+
+def _cached(module: nn.Module, name: str, params: Sequence[torch.Tensor], dtype: torch.dtype, build):
+    """Derived weights cached on `module`, rebuilt when any source parameter changes (in-place
+    updates bump ``_version``; load_state_dict does) or the dtype/device differs."""
+    key = (dtype, params[0].device, tuple(p._version for p in params), tuple(p.data_ptr() for p in params))
+    hit = module.__dict__.get(name)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    with torch.no_grad():
+        val = tuple(t.to(dtype).contiguous() for t in build())
+    module.__dict__[name] = (key, val)
+    return val
+
+
+def _ffn_in_fused(block: nn.Module, proj: nn.Linear, dtype: torch.dtype):
+    """The block's message projection folded into the FFN's first layer (hip path):
+    ffn0(cat(x, proj(m))) = cat(x, m) @ [W_x | W_m·W_p]ᵀ + (b + W_m·b_p), computed in fp32.
+    (lightglue.py:104-106, 181-183: the projection feeds only the FFN.)"""
+    lin = block.ffn[0]
+
+    def build():
+        d = proj.weight.shape[0]
+        w = lin.weight.float()
+        wx, wm = w[:, :d], w[:, d:]
+        return (torch.cat((wx, wm @ proj.weight.float()), 1), lin.bias.float() + wm @ proj.bias.float())
+
+    return _cached(block, "_ffn_in_fused", (lin.weight, lin.bias, proj.weight, proj.bias), dtype, build)
+
+
+def _ffn_tail(block: nn.Module, x: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
+    """x + Linear(GELU(LayerNorm(h))) with LayerNorm+GELU as one gfx950 kernel."""
+    return x + block.ffn[3](_Hip.layernorm_gelu(h, block.ffn[1]))
 
 
 def _ffn_apply(ffn: nn.Sequential, h: torch.Tensor, hip: bool) -> torch.Tensor:
@@ -170,10 +226,10 @@ class SelfBlock(nn.Module):
         return out
 
     def finish(self, x: torch.Tensor, contexts: Sequence[torch.Tensor], hip: bool = False) -> torch.Tensor:
-        if hip:
-            merged = _Hip.merge_heads(*contexts)
-        else:
-            merged = torch.cat([c[0].transpose(0, 1).reshape(c.shape[2], -1) for c in contexts], 0)[None]
+        if hip:  # [x | heads merged] in one pass, out_proj folded into ffn[0]
+            w, b = _ffn_in_fused(self, self.out_proj, x.dtype)
+            return _ffn_tail(self, x, F.linear(_Hip.merge_heads_cat(x, *contexts), w, b))
+        merged = torch.cat([c[0].transpose(0, 1).reshape(c.shape[2], -1) for c in contexts], 0)[None]
         return x + _ffn_apply(self.ffn, torch.cat((x, self.out_proj(merged)), -1), hip)
 
 
@@ -197,11 +253,18 @@ class CrossBlock(nn.Module):
             a += ni
         return out
 
+    def qk_v(self, x: torch.Tensor, splits: Sequence[int]):
+        """hip path: to_qk and to_v as ONE GEMM on stacked weights, heads split from its halves."""
+        w, b = _cached(self, "_qkv_stacked", (self.to_qk.weight, self.to_qk.bias, self.to_v.weight, self.to_v.bias),
+                       x.dtype, lambda: (torch.cat((self.to_qk.weight, self.to_v.weight), 0),
+                                         torch.cat((self.to_qk.bias, self.to_v.bias), 0)))
+        return _Hip.split_heads2_ld(F.linear(x, w, b), self.heads, splits)
+
     def finish(self, x: torch.Tensor, ms: Sequence[torch.Tensor], hip: bool = False) -> torch.Tensor:
-        if hip:
-            merged = _Hip.merge_heads(*ms)
-        else:
-            merged = torch.cat([m[0].transpose(0, 1).reshape(m.shape[2], -1) for m in ms], 0)[None]
+        if hip:  # [x | heads merged] in one pass, to_out folded into ffn[0]
+            w, b = _ffn_in_fused(self, self.to_out, x.dtype)
+            return _ffn_tail(self, x, F.linear(_Hip.merge_heads_cat(x, *ms), w, b))
+        merged = torch.cat([m[0].transpose(0, 1).reshape(m.shape[2], -1) for m in ms], 0)[None]
         return x + _ffn_apply(self.ffn, torch.cat((x, self.to_out(merged)), -1), hip)
 
 
@@ -216,7 +279,7 @@ class TransformerLayer(nn.Module):
         sa, ca = self.self_attn, self.cross_attn
         x = sa.finish(x, attention(sa.qkv(x, cos, sin, splits, hip)), hip)   # one grouped launch (self0, self1)
         if hip:
-            (qk0, qk1), (v0, v1) = _Hip.split_heads2(ca.to_qk(x), ca.to_v(x), ca.heads, splits)
+            (qk0, qk1), (v0, v1) = ca.qk_v(x, splits)
         else:
             qk0, qk1 = ca.heads_of(ca.to_qk(x), splits)
             v0, v1 = ca.heads_of(ca.to_v(x), splits)

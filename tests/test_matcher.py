@@ -168,6 +168,18 @@ def test_glue_kernels_match_torch(dtype):
             assert torch.equal(r, g_)
         merged = mt._Hip.merge_heads(a0, a1)
         assert torch.equal(merged, a)
+        # strided split of one [a | b] projection; [x | merge] concatenation
+        ab = torch.cat((a, b), -1).contiguous()
+        (c0, c1), (d0_, d1_) = mt._Hip.split_heads2_ld(ab, h, (n0, n1))
+        for r, g_ in zip((a0, a1, b0, b1), (c0, c1, d0_, d1_)):
+            assert torch.equal(r, g_)
+        assert torch.equal(mt._Hip.merge_heads_cat(b, a0, a1), torch.cat((b, a), -1))
+        # out_proj folded into ffn[0] (fp32 fold of the weights): same pre-activation
+        w, bias = mt._ffn_in_fused(blk, blk.out_proj, dt)
+        xm = torch.cat((x, a), -1)
+        ref_h = blk.ffn[0](torch.cat((x, blk.out_proj(a)), -1)).float()
+        got_h = torch.nn.functional.linear(xm, w, bias).float()
+        assert float((ref_h - got_h).abs().max()) <= (5e-2 if dtype == "float16" else 1e-4)
         ln = torch.nn.LayerNorm(512).to(dev, dt)
         with torch.no_grad():
             ln.weight.copy_(rnd(512) * 0.1 + 1)

@@ -51,6 +51,34 @@ __global__ __launch_bounds__(NT) void stream_kernel(const u32x4* K, const u32x4*
     O[(size_t)blockIdx.x * NT + threadIdx.x] = acc;
 }
 
+// The same volume by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per instruction) into a 16 KiB
+// per-wave LDS region (overwritten in turn: only the transfer rate is of interest).
+template <int KPW>
+__global__ __launch_bounds__(512) void dma_kernel(const u32x4* K, const u32x4* V, u32x4* O, int span) {
+    __shared__ __attribute__((aligned(16))) char lds[8 * 16384];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int xcd = blockIdx.x & 7, idx = blockIdx.x >> 3;
+    const int per_xcd = gridDim.x >> 3;
+    const int head = xcd >> 1;
+    const int local = (xcd & 1) * per_xcd + idx;
+    const int split = local % (1024 / span);
+    const int key0 = split * span + wave * KPW;
+    const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc((void*)(K + (size_t)head * 1024 * 8), (short)0, 1 << 17, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc((void*)(V + (size_t)head * 1024 * 8), (short)0, 1 << 17, 0x00020000);
+    constexpr int N = KPW / 8;  // 1 KiB pieces per tensor
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (__attribute__((address_space(3))) void*)(lds + wave * 16384 + (i & 15) * 1024), 16,
+                                                 (unsigned)(key0 * 128 + lane * 16), i * 1024, 0, 0);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(vr, (__attribute__((address_space(3))) void*)(lds + wave * 16384 + ((i + N) & 15) * 1024), 16,
+                                                 (unsigned)(key0 * 128 + lane * 16), i * 1024, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    O[(size_t)blockIdx.x * 512 + threadIdx.x] = *(const u32x4*)(lds + threadIdx.x * 16);
+}
+
 __global__ void empty_kernel() {}
 
 template <typename F>
@@ -103,6 +131,10 @@ int main() {
     RUN("nosplit16_256x1024_kpw64_us", 256, 1024, 64, 1024); // 16 rows x 1024 keys: 256 KiB/CU
     RUN("nosplit_128x1024_kpw64_us", 128, 1024, 64, 1024);   // 32 rows x 1024 keys, 16 waves
     RUN("nosplit_64x512_kpw128_us", 64, 512, 128, 1024);     // 64 rows x 1024 keys per WG
+    printf(", \"dma_nosplit_128x512_kpw128_us\": %.3f",
+           time_graph([&] { dma_kernel<128><<<128, 512, 0, s>>>(K, V, O, 1024); }, s, C));
+    printf(", \"dma_split2_256x512_kpw64_us\": %.3f",
+           time_graph([&] { dma_kernel<64><<<256, 512, 0, s>>>(K, V, O, 512); }, s, C));
     printf("}\n");
     return 0;
 }
