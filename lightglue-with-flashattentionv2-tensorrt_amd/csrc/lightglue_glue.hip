@@ -157,11 +157,27 @@ __global__ __launch_bounds__(256) void ln_gelu_kernel(const T* __restrict__ x, c
 }
 
 // ---- dual log-softmax ----
-// pass 1: blocks [0, rb) -> row logsumexp (one wave per row); blocks [rb, ...) -> column
-// logsumexp (one thread per column, online max/sum down the rows; consecutive threads read
-// consecutive columns of a row: coalesced).
+// Pass 1 (lse_kernel): blocks [0, rb) -> row logsumexp (one wave per row); blocks [rb, ...) ->
+// column partials: a block is 64 consecutive columns x one chunk of kColChunk rows, its 256
+// threads = 64 columns x 4 interleaved rows (a wave reads 256 contiguous bytes of a row), online
+// (max, sum) per thread, merged through LDS, one (max, sum) per (chunk, column) to the workspace.
+// Pass 2 (dual_combine_kernel): a block is 8 rows x 256 columns; it first finishes the column
+// logsumexp of its 256 columns from the chunk partials, then writes its rows.
+constexpr int kColChunk = 128;  // rows per column-partial block
+constexpr int kCombRows = 8;    // rows per combine block
+
+__device__ __forceinline__ void lse_merge(float& mx, float& s, float m2, float s2) {
+    if (m2 == -INFINITY) return;
+    if (m2 > mx) {
+        s = s * __expf(mx - m2) + s2;
+        mx = m2;
+    } else {
+        s += s2 * __expf(m2 - mx);
+    }
+}
+
 __global__ __launch_bounds__(256) void lse_kernel(const float* __restrict__ sim, int m, int n, int rb,
-                                                  float* lse_row, float* lse_col) {
+                                                  float* lse_row, float2* col_part) {
     if ((int)blockIdx.x < rb) {
         const int lane = threadIdx.x & 63;
         const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -174,11 +190,17 @@ __global__ __launch_bounds__(256) void lse_kernel(const float* __restrict__ sim,
         for (int j = lane; j < n; j += 64) s += __expf(r[j] - mx);
         s = wave_sum(s);
         if (lane == 0) lse_row[row] = mx + __logf(s);
-    } else {
-        const int col = (blockIdx.x - rb) * blockDim.x + threadIdx.x;
-        if (col >= n) return;
-        float mx = -INFINITY, s = 0.f;
-        for (int i = 0; i < m; ++i) {
+        return;
+    }
+    __shared__ float2 part[4][64];
+    const int b = blockIdx.x - rb, cgroups = (n + 63) / 64;
+    const int chunk = b / cgroups, col = (b % cgroups) * 64 + (threadIdx.x & 63);
+    const int r4 = threadIdx.x >> 6;
+    const int i0 = chunk * kColChunk, i1 = min(m, i0 + kColChunk);
+    float mx = -INFINITY, s = 0.f;
+    if (col < n) {
+#pragma unroll 4
+        for (int i = i0 + r4; i < i1; i += 4) {
             const float v = sim[(size_t)i * n + col];
             if (v > mx) {
                 s = s * __expf(mx - v) + 1.f;
@@ -187,7 +209,13 @@ __global__ __launch_bounds__(256) void lse_kernel(const float* __restrict__ sim,
                 s += __expf(v - mx);
             }
         }
-        lse_col[col] = mx + __logf(s);
+    }
+    part[r4][threadIdx.x & 63] = make_float2(mx, s);
+    __syncthreads();
+    if (r4 == 0 && col < n) {
+#pragma unroll
+        for (int k = 1; k < 4; ++k) lse_merge(mx, s, part[k][threadIdx.x].x, part[k][threadIdx.x].y);
+        col_part[(size_t)chunk * n + col] = make_float2(mx, s);
     }
 }
 
@@ -196,11 +224,22 @@ __device__ __forceinline__ float log_sigmoid(float z) { return fminf(z, 0.f) - l
 // pass 2: scores = 2 sim - lse_row[i] - lse_col[j] + logsig(z0[i]) + logsig(z1[j])
 __global__ __launch_bounds__(256) void dual_combine_kernel(const float* __restrict__ sim, const float* z0,
                                                            const float* z1, const float* lse_row,
-                                                           const float* lse_col, int m, int n, float* out) {
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (long)m * n) return;
-    const int i = idx / n, j = idx - (long)i * n;
-    out[idx] = 2.f * sim[idx] - lse_row[i] - lse_col[j] + log_sigmoid(z0[i]) + log_sigmoid(z1[j]);
+                                                           const float2* col_part, int chunks, int m, int n,
+                                                           float* out) {
+    const int cblocks = (n + 255) / 256;
+    const int j = (blockIdx.x % cblocks) * 256 + threadIdx.x;
+    const int i0 = (blockIdx.x / cblocks) * kCombRows;
+    if (j >= n) return;
+    float mx = -INFINITY, s = 0.f;
+    for (int c = 0; c < chunks; ++c) {
+        const float2 p = col_part[(size_t)c * n + j];
+        lse_merge(mx, s, p.x, p.y);
+    }
+    const float cterm = logf(s) + mx;
+    const float zj = log_sigmoid(z1[j]);
+    const int i1 = min(m, i0 + kCombRows);
+    for (int i = i0; i < i1; ++i)
+        out[(size_t)i * n + j] = 2.f * sim[(size_t)i * n + j] - lse_row[i] - cterm + log_sigmoid(z0[i]) + zj;
 }
 
 inline unsigned blocks_for(long threads) { return (unsigned)((threads + 255) / 256); }
@@ -319,7 +358,9 @@ int32_t lg_layernorm_gelu(int32_t dtype, const void* x, const void* gamma, const
 }
 
 size_t lg_log_double_softmax_workspace(int32_t m, int32_t n) {
-    return (size_t)((m > 0 ? m : 0) + (n > 0 ? n : 0)) * sizeof(float);
+    if (m <= 0 || n <= 0) return 0;
+    const size_t chunks = (size_t)(m + kColChunk - 1) / kColChunk;
+    return ((size_t)m * sizeof(float) + 15) / 16 * 16 + chunks * (size_t)n * sizeof(float2);
 }
 
 int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1, int32_t m, int32_t n, float* scores,
@@ -328,11 +369,15 @@ int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1
         return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_log_double_softmax", "bad arguments");
     if (m == 0 || n == 0) return MHA_HD64_STATUS_SUCCESS;
     float* lse_row = reinterpret_cast<float*>(workspace);
-    float* lse_col = lse_row + m;
+    float2* col_part = reinterpret_cast<float2*>(reinterpret_cast<char*>(workspace) +
+                                                 ((size_t)m * sizeof(float) + 15) / 16 * 16);
     const int rb = (m + 3) / 4;
-    hipLaunchKernelGGL(lse_kernel, dim3(rb + blocks_for(n)), dim3(256), 0, stream, sim, m, n, rb, lse_row, lse_col);
-    hipLaunchKernelGGL(dual_combine_kernel, dim3(blocks_for((long)m * n)), dim3(256), 0, stream, sim, z0, z1, lse_row,
-                       lse_col, m, n, scores);
+    const int chunks = (m + kColChunk - 1) / kColChunk;
+    const int cblocks = (n + 63) / 64;
+    hipLaunchKernelGGL(lse_kernel, dim3(rb + chunks * cblocks), dim3(256), 0, stream, sim, m, n, rb, lse_row,
+                       col_part);
+    hipLaunchKernelGGL(dual_combine_kernel, dim3(((m + kCombRows - 1) / kCombRows) * ((n + 255) / 256)), dim3(256), 0,
+                       stream, sim, z0, z1, lse_row, col_part, chunks, m, n, scores);
     return launched("lg_log_double_softmax");
 }
 

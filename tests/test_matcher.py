@@ -188,9 +188,10 @@ def test_glue_kernels_match_torch(dtype):
         ref = torch.nn.functional.gelu(ln(hx).float()).to(dt)
         tol_ln = 2e-2 if dtype == "float16" else 1e-4
         assert float((mt._Hip.layernorm_gelu(hx, ln).float() - ref.float()).abs().max()) <= tol_ln
-        sim = rnd(1, 130, 211).float() * 5
-        z0, z1 = rnd(1, 130, 1).float(), rnd(1, 211, 1).float()
-        ref = mt.log_double_softmax(sim, z0, z1)
-        got = mt._Hip.log_double_softmax(sim, z0, z1)
-        torch.cuda.synchronize()
-        assert float((ref - got).abs().max()) <= 1e-4
+        for m_, n_ in ((130, 211), (1024, 777), (1, 2000), (2000, 5)):  # column pass: 128-row chunks
+            sim = rnd(1, m_, n_).float() * 5
+            z0, z1 = rnd(1, m_, 1).float(), rnd(1, n_, 1).float()
+            ref = mt.log_double_softmax(sim, z0, z1)
+            got = mt._Hip.log_double_softmax(sim, z0, z1)
+            torch.cuda.synchronize()
+            assert float((ref - got).abs().max()) <= 1e-4, (m_, n_)
