@@ -54,6 +54,27 @@ int32_t lg_merge_heads_cat(int32_t dtype, const void* x, const void* x0, const v
 int32_t lg_layernorm_gelu(int32_t dtype, const void* x, const void* gamma, const void* beta, int32_t rows,
                           int32_t dim, float eps, void* y, hipStream_t stream);
 
+/* ---- projections with their neighbours fused (fp16 only; csrc/lightglue_linear.hip) ----
+ * W [n, k] row-major (nn.Linear layout), bias [n]; k in {256, 512}; n a multiple of 64; rows m
+ * any. A/W/x/ctx 16-byte aligned, bias/out/res/cos/sin 8-byte aligned.
+ * lg_linear:            out [m, n] = A [m, k] · Wᵀ + bias (+ res [m, n] when res != NULL). */
+int32_t lg_linear(const void* a, const void* w, const void* bias, const void* res, int32_t m, int32_t n, int32_t k,
+                  void* out, hipStream_t stream);
+/* lg_linear_cat:        out [n0+n1, n] = [x | merge_heads(ctx0, ctx1)] · Wᵀ + bias with x [n0+n1, heads*64],
+ *                       ctx_i [heads, ni, 64] (k = 2*heads*64; the FFN input of lightglue.py:104/181). */
+int32_t lg_linear_cat(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
+                      const void* w, const void* bias, int32_t n, void* out, hipStream_t stream);
+/* lg_linear_qkv_rotary: SelfBlock projection (lightglue.py:111-134) with W's rows and the bias in
+ *                       [q|k|v][head][dim] order (row j*heads*64 + h*64 + d = Wqkv row (h*64+d)*3 + j):
+ *                       rotary (cos/sin [n0+n1, 64]) on q and k, per-image head-major outputs. */
+int32_t lg_linear_qkv_rotary(const void* x, const void* w_perm, const void* b_perm, const void* cos, const void* sin,
+                             int32_t heads, int32_t n0, int32_t n1, int32_t k, void* q0, void* k0, void* v0, void* q1,
+                             void* k1, void* v1, hipStream_t stream);
+/* lg_linear_split2:     CrossBlock to_qk | to_v as one projection (W = [W_qk; W_v], lightglue.py:158-166):
+ *                       per-image head-major a (= qk) and b (= v). */
+int32_t lg_linear_split2(const void* x, const void* w, const void* bias, int32_t heads, int32_t n0, int32_t n1,
+                         int32_t k, void* a0, void* a1, void* b0, void* b1, hipStream_t stream);
+
 /* sigmoid_log_double_softmax (lightglue.py:197-205), fp32: scores[i][j] = 2 sim[i][j]
  * - logsumexp_j' sim[i][j'] - logsumexp_i' sim[i'][j] + logsigmoid(z0[i]) + logsigmoid(z1[j]).
  * sim, scores [m, n]; z0 [m], z1 [n]; workspace >= lg_log_double_softmax_workspace(m, n) bytes. */

@@ -1,0 +1,279 @@
+// lightglue_linear.hip — the matcher's projections as gfx950 MFMA kernels with their neighbours
+// fused in (include/lightglue_glue.h, lg_linear_*). fp16 in/out, fp32 accumulation.
+//
+// The LightGlue layer (lightglue_pytorch_no_plugin/lightglue.py:88-194) is a chain of small
+// GEMMs (M = both images' keypoints, K = 256 or 512, N = 256..768) separated by layout and
+// elementwise steps; at matcher sizes every one of them is a few-microsecond, latency-bound
+// launch. These kernels do the GEMM and the step either side in one launch:
+//   * lg_linear           : out = A·Wᵀ + b (+ residual)                  (FFN layers, residual add)
+//   * lg_linear_cat       : A = [x | merge_heads(ctx0, ctx1)] gathered on load (FFN input of
+//                           both blocks, lightglue.py:104/181; the message projection is folded
+//                           into W by the caller)
+//   * lg_linear_qkv_rotary: SelfBlock Wqkv + rotary + per-image head-major q/k/v (:111-134; W's
+//                           rows pre-permuted to [q|k|v][head][dim] order by the caller)
+//   * lg_linear_split2    : CrossBlock to_qk | to_v as one GEMM + per-image head split (:158-166)
+//
+// Workgroup: 64 rows (m) x 64 output channels (n), 4 waves as 2 x 2 tiles of 32 x 32. The
+// product is computed transposed, Cᵀ = W·Aᵀ on v_mfma_f32_32x32x16_f16 (A-operand = W rows,
+// B-operand = activation rows, both K-contiguous), so a lane ends up owning one activation row
+// and 4 runs of 4 consecutive output channels: epilogue stores are 8-B row segments and a rotary
+// pair (2d, 2d+1) sits in one lane. Both 64 x K tiles reach LDS by LDS-DMA in 128-column
+// chunks ([chunk][row][256 B], 16-B units XOR-swizzled by row & 15 on the source address:
+// conflict-free ds_read_b128 of 16 rows at one k); the MFMAs of chunk c start once c has
+// landed (counted vmcnt + barrier) while the later chunks stream in.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lightglue_glue.h"
+#include "mha_hd64.h"
+#include "mha_hd64_internal.h"
+
+namespace {
+
+typedef _Float16 f16;
+typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+typedef f16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) char lds_char;
+typedef __attribute__((address_space(3))) f16x8 lds_f16x8;
+
+constexpr int kBM = 64, kBN = 64, kKC = 128;  // tile rows, tile channels, K columns per LDS chunk
+constexpr int kChunkBytes = 64 * kKC * 2;     // one [64 rows][128 k] fp16 chunk = 16 KiB
+constexpr int kD = 64;                        // head dim
+
+enum { EPI_BIAS = 0, EPI_QKV_ROTARY = 1, EPI_SPLIT2 = 2 };
+
+struct LinArgs {
+    const f16* a;      // [m, k] activations (A-gather: x [m, k/2])
+    const f16* ctx0;   // A-gather: head-major attention outputs of image 0 / 1 [heads, ni, 64]
+    const f16* ctx1;
+    const f16* w;      // [n, k]
+    const f16* bias;   // [n]
+    const f16* res;    // [m, n] residual (EPI_BIAS, nullable)
+    const f16* cosv;   // [m, 64] rotary tables (EPI_QKV_ROTARY)
+    const f16* sinv;
+    f16* out[6];       // EPI_BIAS: out[0] [m, n]; QKV: q0 k0 v0 q1 k1 v1; SPLIT2: a0 a1 b0 b1
+    int m, n, k;
+    int heads, n0;     // per-image split (n0 rows of image 0; m - n0 of image 1)
+    int mtiles, total;
+};
+
+// global source of A row `row`, 16-B unit `gc` (8 k values)
+template <bool GATHER>
+__device__ __forceinline__ const f16* a_src(const LinArgs& p, int row, int gc) {
+    if constexpr (!GATHER) {
+        return p.a + (size_t)row * p.k + gc * 8;
+    } else {
+        const int half = p.k / 2, col = gc * 8;
+        if (col < half) return p.a + (size_t)row * half + col;  // x
+        const int c2 = col - half, h = c2 / kD, d = c2 % kD;
+        const bool first = row < p.n0;
+        const int r = first ? row : row - p.n0, nn = first ? p.n0 : p.m - p.n0;
+        return (first ? p.ctx0 : p.ctx1) + ((size_t)h * nn + r) * kD + d;
+    }
+}
+
+template <int EPI, bool GATHER, int KC>
+__global__ __launch_bounds__(256) void linear_kernel(LinArgs p) {
+    static_assert(KC == 2 || KC == 4, "k = 256 or 512");
+    __shared__ __attribute__((aligned(16))) char smem[2 * KC * kChunkBytes];  // W, A tiles (64 / 128 KiB)
+    lds_char* const lds = (lds_char*)smem;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave & 1, wn = wave >> 1;  // this wave's 32 x 32 tile of the 64 x 64
+    const int r = lane & 31, hh = lane >> 5;
+    // XCD-aware order: consecutive j (one XCD) = consecutive m tiles of one n tile (W tile in L2)
+    int j;
+    {
+        const int T = p.total, L = blockIdx.x, q8 = T >> 3, r8 = T & 7, xcd = L & 7;
+        j = xcd * q8 + min(xcd, r8) + (L >> 3);
+    }
+    const int mt = j % p.mtiles, nt = j / p.mtiles;
+    const int m0 = mt * kBM, n0 = nt * kBN;
+    const unsigned wbase = 0, abase = KC * kChunkBytes;
+    const int wrow = wn * 32 + r, arow = wm * 32 + r;
+    const int m = min(m0 + arow, p.m - 1);  // this lane's output row (clamped; stores are guarded)
+
+    // Epilogue operands first (plain loads, older than every DMA below, so the counted waits
+    // of the main loop stay exact): bias, residual / rotary tables of the lane's 4 x 4 channels.
+    f16x4 bias4[4], aux0[4], aux1[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * 32 + 8 * g + 4 * hh;
+        bias4[g] = *reinterpret_cast<const f16x4*>(p.bias + n);
+        if constexpr (EPI == EPI_BIAS) {
+            if (p.res) aux0[g] = *reinterpret_cast<const f16x4*>(p.res + (size_t)m * p.n + n);
+        } else if constexpr (EPI == EPI_QKV_ROTARY) {
+            aux0[g] = *reinterpret_cast<const f16x4*>(p.cosv + (size_t)m * kD + n % kD);
+            aux1[g] = *reinterpret_cast<const f16x4*>(p.sinv + (size_t)m * kD + n % kD);
+        }
+    }
+
+    __builtin_amdgcn_sched_barrier(0);  // (they stay ahead of the DMAs)
+
+    // ---- loads: per chunk c, W rows n0.. and A rows m0.. ; one DMA = 4 rows x 256 B ----
+    // lane -> (row 4i + lane/16, LDS unit lane%16 <- global unit (lane%16) ^ (row & 15))
+    // Wave w issues DMA instructions i = w, w+4, w+8, w+12 of each 16-instruction chunk tile.
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int i = wave + 4 * s;
+            const int row = 4 * i + (lane >> 4), pu = lane & 15;
+            const int gc = c * (kKC / 8) + (pu ^ (row & 15));
+            const int wr = min(n0 + row, p.n - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(p.w + (size_t)wr * p.k + gc * 8),
+                                             (__attribute__((address_space(3))) void*)(smem + wbase + c * kChunkBytes + i * 1024),
+                                             16, 0, 0);
+            const int ar = min(m0 + row, p.m - 1);
+            __builtin_amdgcn_global_load_lds((const void*)a_src<GATHER>(p, ar, gc),
+                                             (__attribute__((address_space(3))) void*)(smem + abase + c * kChunkBytes + i * 1024),
+                                             16, 0, 0);
+        }
+    }
+
+    f32x16 acc = {};
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+        // chunk c landed for this wave's DMAs (8 per chunk, in issue order), then for everyone's
+        switch (KC - 1 - c) {
+            case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+            case 1: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+            case 2: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+            default: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+        }
+        __builtin_amdgcn_s_barrier();
+        const unsigned wc = wbase + c * kChunkBytes + wrow * 256, ac = abase + c * kChunkBytes + arow * 256;
+        // all 8 k-steps' fragments of the chunk first (one LDS latency per chunk, not per step)
+        f16x8 wf[kKC / 16], af[kKC / 16];
+#pragma unroll
+        for (int s = 0; s < kKC / 16; ++s) {
+            const int u = 2 * s + hh;  // 16-B unit of the k-step
+            wf[s] = *(lds_f16x8*)(lds + wc + ((u ^ (wrow & 15)) << 4));
+            af[s] = *(lds_f16x8*)(lds + ac + ((u ^ (arow & 15)) << 4));
+        }
+#pragma unroll
+        for (int s = 0; s < kKC / 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[s], af[s], acc, 0, 0, 0);
+    }
+
+    // ---- epilogue: lane = activation row m; acc[4g + t] = channel n0 + wn*32 + 8g + 4hh + t ----
+    if (m0 + arow >= p.m) return;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * 32 + 8 * g + 4 * hh;  // 4 consecutive channels n..n+3
+        float v[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = acc[4 * g + t] + (float)bias4[g][t];
+        if constexpr (EPI == EPI_BIAS) {
+            if (p.res) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) v[t] += (float)aux0[g][t];
+            }
+            *reinterpret_cast<f16x4*>(p.out[0] + (size_t)m * p.n + n) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+        } else {
+            const int hd = p.heads * kD;
+            const int part = n / hd, h = (n % hd) / kD, d = n % kD;
+            const bool first = m < p.n0;
+            const int row = first ? m : m - p.n0, nn = first ? p.n0 : p.m - p.n0;
+            if constexpr (EPI == EPI_QKV_ROTARY) {
+                if (part < 2) {  // q, k: (x0, x1) -> (x0 c - x1 s, x1 c + x0 s), pairs (d, d+1)
+                    const f16x4 cc = aux0[g], ss = aux1[g];
+#pragma unroll
+                    for (int t = 0; t < 4; t += 2) {
+                        const float x0 = v[t], x1 = v[t + 1];
+                        v[t] = x0 * (float)cc[t] - x1 * (float)ss[t];
+                        v[t + 1] = x1 * (float)cc[t + 1] + x0 * (float)ss[t + 1];
+                    }
+                }
+            }
+            f16* dst = p.out[(first ? 0 : (EPI == EPI_QKV_ROTARY ? 3 : 1)) + (EPI == EPI_QKV_ROTARY ? part : 2 * part)];
+            *reinterpret_cast<f16x4*>(dst + ((size_t)h * nn + row) * kD + d) =
+                f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+        }
+    }
+}
+
+template <int EPI, bool GATHER>
+int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
+    p.mtiles = (p.m + kBM - 1) / kBM;
+    p.total = p.mtiles * (p.n / kBN);
+    if (p.k == 256)
+        hipLaunchKernelGGL((linear_kernel<EPI, GATHER, 2>), dim3(p.total), dim3(256), 0, stream, p);
+    else
+        hipLaunchKernelGGL((linear_kernel<EPI, GATHER, 4>), dim3(p.total), dim3(256), 0, stream, p);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
+                           : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, what, hipGetErrorString(e));
+}
+
+bool aligned16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+bool aligned8(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 7) == 0; }
+bool shape_ok(int m, int n, int k) { return m >= 0 && n > 0 && n % kBN == 0 && (k == 256 || k == 512); }
+
+int32_t bad(const char* what) { return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, what, "bad arguments"); }
+
+}  // namespace
+
+extern "C" {
+
+int32_t lg_linear(const void* a, const void* w, const void* bias, const void* res, int32_t m, int32_t n, int32_t k,
+                  void* out, hipStream_t stream) {
+    if (!shape_ok(m, n, k) || !a || !w || !bias || !out || !aligned16(a) || !aligned16(w) || !aligned8(bias) ||
+        !aligned8(out) || (res && !aligned8(res)))
+        return bad("lg_linear");
+    if (m == 0) return MHA_HD64_STATUS_SUCCESS;
+    LinArgs p{};
+    p.a = (const f16*)a, p.w = (const f16*)w, p.bias = (const f16*)bias, p.res = (const f16*)res;
+    p.out[0] = (f16*)out;
+    p.m = m, p.n = n, p.k = k, p.n0 = m;
+    return launch<EPI_BIAS, false>(p, stream, "lg_linear");
+}
+
+int32_t lg_linear_cat(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
+                      const void* w, const void* bias, int32_t n, void* out, hipStream_t stream) {
+    const int k = 2 * heads * kD, m = n0 + n1;
+    if (heads <= 0 || n0 < 0 || n1 < 0 || !shape_ok(m, n, k) || !x || !w || !bias || !out || !aligned16(x) ||
+        (n0 && !aligned16(ctx0)) || (n1 && !aligned16(ctx1)) || !aligned16(w) || !aligned8(bias) || !aligned8(out))
+        return bad("lg_linear_cat");
+    if (m == 0) return MHA_HD64_STATUS_SUCCESS;
+    LinArgs p{};
+    p.a = (const f16*)x, p.ctx0 = (const f16*)ctx0, p.ctx1 = (const f16*)ctx1, p.w = (const f16*)w;
+    p.bias = (const f16*)bias, p.out[0] = (f16*)out;
+    p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0;
+    return launch<EPI_BIAS, true>(p, stream, "lg_linear_cat");
+}
+
+int32_t lg_linear_qkv_rotary(const void* x, const void* w_perm, const void* b_perm, const void* cosv,
+                             const void* sinv, int32_t heads, int32_t n0, int32_t n1, int32_t k, void* q0, void* k0,
+                             void* v0, void* q1, void* k1, void* v1, hipStream_t stream) {
+    const int m = n0 + n1, n = 3 * heads * kD;
+    if (heads <= 0 || n0 < 0 || n1 < 0 || !shape_ok(m, n, k) || !x || !w_perm || !b_perm || !cosv || !sinv ||
+        !aligned16(x) || !aligned16(w_perm) || !aligned8(b_perm) || !aligned8(cosv) || !aligned8(sinv))
+        return bad("lg_linear_qkv_rotary");
+    if (m == 0) return MHA_HD64_STATUS_SUCCESS;
+    LinArgs p{};
+    p.a = (const f16*)x, p.w = (const f16*)w_perm, p.bias = (const f16*)b_perm;
+    p.cosv = (const f16*)cosv, p.sinv = (const f16*)sinv;
+    f16* outs[6] = {(f16*)q0, (f16*)k0, (f16*)v0, (f16*)q1, (f16*)k1, (f16*)v1};
+    for (int i = 0; i < 6; ++i) p.out[i] = outs[i];
+    p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0;
+    return launch<EPI_QKV_ROTARY, false>(p, stream, "lg_linear_qkv_rotary");
+}
+
+int32_t lg_linear_split2(const void* x, const void* w, const void* bias, int32_t heads, int32_t n0, int32_t n1,
+                         int32_t k, void* a0, void* a1, void* b0, void* b1, hipStream_t stream) {
+    const int m = n0 + n1, n = 2 * heads * kD;
+    if (heads <= 0 || n0 < 0 || n1 < 0 || !shape_ok(m, n, k) || !x || !w || !bias || !aligned16(x) ||
+        !aligned16(w) || !aligned8(bias))
+        return bad("lg_linear_split2");
+    if (m == 0) return MHA_HD64_STATUS_SUCCESS;
+    LinArgs p{};
+    p.a = (const f16*)x, p.w = (const f16*)w, p.bias = (const f16*)bias;
+    f16* outs[4] = {(f16*)a0, (f16*)a1, (f16*)b0, (f16*)b1};
+    for (int i = 0; i < 4; ++i) p.out[i] = outs[i];
+    p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0;
+    return launch<EPI_SPLIT2, false>(p, stream, "lg_linear_split2");
+}
+
+}  // extern "C"

@@ -93,6 +93,49 @@ class _Hip:
         _check(st, "lg_merge_heads_cat")
         return out
 
+    # ---- projections with their neighbours fused (fp16; csrc/lightglue_linear.hip) ----
+    @staticmethod
+    def linear(a, w, b, res=None):
+        """a [1, M, K] -> a·wᵀ + b (+ res) [1, M, N]."""
+        m, k = a.shape[1], a.shape[2]
+        out = torch.empty((1, m, w.shape[0]), dtype=a.dtype, device=a.device)
+        st = _lib.load().lg_linear(a.data_ptr(), w.data_ptr(), b.data_ptr(), res.data_ptr() if res is not None else None,
+                                   m, w.shape[0], k, out.data_ptr(), _Hip._stream(a))
+        _check(st, "lg_linear")
+        return out
+
+    @staticmethod
+    def linear_cat(x, c0, c1, w, b):
+        """[x | merge_heads(c0, c1)]·wᵀ + b."""
+        heads, n0, n1 = c0.shape[1], c0.shape[2], c1.shape[2]
+        out = torch.empty((1, n0 + n1, w.shape[0]), dtype=x.dtype, device=x.device)
+        st = _lib.load().lg_linear_cat(x.data_ptr(), c0.data_ptr(), c1.data_ptr(), heads, n0, n1, w.data_ptr(),
+                                       b.data_ptr(), w.shape[0], out.data_ptr(), _Hip._stream(x))
+        _check(st, "lg_linear_cat")
+        return out
+
+    @staticmethod
+    def linear_qkv_rotary(x, w_perm, b_perm, cos, sin, heads, splits):
+        n0, n1 = splits
+        mk = lambda n: torch.empty((1, heads, n, 64), dtype=x.dtype, device=x.device)  # noqa: E731
+        out = [tuple(mk(n) for _ in range(3)) for n in (n0, n1)]
+        st = _lib.load().lg_linear_qkv_rotary(x.data_ptr(), w_perm.data_ptr(), b_perm.data_ptr(), cos.data_ptr(),
+                                              sin.data_ptr(), heads, n0, n1, x.shape[2],
+                                              *(t.data_ptr() for t in out[0]), *(t.data_ptr() for t in out[1]),
+                                              _Hip._stream(x))
+        _check(st, "lg_linear_qkv_rotary")
+        return out
+
+    @staticmethod
+    def linear_split2(x, w, b, heads, splits):
+        n0, n1 = splits
+        mk = lambda n: torch.empty((1, heads, n, 64), dtype=x.dtype, device=x.device)  # noqa: E731
+        a0, a1, b0, b1 = mk(n0), mk(n1), mk(n0), mk(n1)
+        st = _lib.load().lg_linear_split2(x.data_ptr(), w.data_ptr(), b.data_ptr(), heads, n0, n1, x.shape[2],
+                                          a0.data_ptr(), a1.data_ptr(), b0.data_ptr(), b1.data_ptr(), _Hip._stream(x))
+        _check(st, "lg_linear_split2")
+        return (a0, a1), (b0, b1)
+
     @staticmethod
     def merge_heads(x0, x1):
         heads, n0, n1 = x0.shape[1], x0.shape[2], x1.shape[2]
@@ -150,6 +193,26 @@ def _ffn_in_fused(block: nn.Module, proj: nn.Linear, dtype: torch.dtype):
         return (torch.cat((wx, wm @ proj.weight.float()), 1), lin.bias.float() + wm @ proj.bias.float())
 
     return _cached(block, "_ffn_in_fused", (lin.weight, lin.bias, proj.weight, proj.bias), dtype, build)
+
+
+def _qkv_perm(block: nn.Module, dtype: torch.dtype):
+    """Wqkv's rows and bias in [q|k|v][head][dim] order (lg_linear_qkv_rotary's layout): new row
+    j*H*64 + h*64 + d = reference row (h*64 + d)*3 + j (lightglue.py:111-114)."""
+    lin = block.Wqkv
+
+    def build():
+        hd = block.heads * block.head_dim
+        new = torch.arange(3 * hd, device=lin.weight.device)
+        j, hd_idx = new // hd, new % hd
+        old = hd_idx * 3 + j
+        return lin.weight[old], lin.bias[old]
+
+    return _cached(block, "_qkv_perm", (lin.weight, lin.bias), dtype, build)
+
+
+def _fused_ok(x: torch.Tensor, block: nn.Module) -> bool:
+    """The fused-projection kernels: fp16, 4 x 64 heads (k = 256 / 512)."""
+    return x.dtype == torch.float16 and block.heads * block.head_dim == 256 and x.shape[-1] == 256
 
 
 def _ffn_tail(block: nn.Module, x: torch.Tensor, h: torch.Tensor) -> torch.Tensor:
@@ -277,6 +340,8 @@ class TransformerLayer(nn.Module):
     def forward(self, x, cos, sin, splits, attention: AttnFn, hip: bool = False):
         """x: both images' descriptors [1, N0+N1, d] (image 0 rows first)."""
         sa, ca = self.self_attn, self.cross_attn
+        if hip and _fused_ok(x, sa):
+            return self._forward_fused(x, cos, sin, splits, attention)
         x = sa.finish(x, attention(sa.qkv(x, cos, sin, splits, hip)), hip)   # one grouped launch (self0, self1)
         if hip:
             (qk0, qk1), (v0, v1) = ca.qk_v(x, splits)
@@ -284,6 +349,27 @@ class TransformerLayer(nn.Module):
             qk0, qk1 = ca.heads_of(ca.to_qk(x), splits)
             v0, v1 = ca.heads_of(ca.to_v(x), splits)
         return ca.finish(x, attention([(qk0, qk1, v1), (qk1, qk0, v0)]), hip)  # one grouped launch (cross)
+
+
+    def _forward_fused(self, x, cos, sin, splits, attention: AttnFn):
+        """fp16 hip path: 5 launches per block -- projection(+rotary/head split), grouped
+        attention, FFN input projection gathering [x | heads] (message projection folded in),
+        LayerNorm+GELU, FFN output projection + residual."""
+        sa, ca = self.self_attn, self.cross_attn
+        wq, bq = _qkv_perm(sa, x.dtype)
+        qkv = _Hip.linear_qkv_rotary(x, wq, bq, cos, sin, sa.heads, splits)
+        c0, c1 = attention(qkv)                                          # self0, self1: one launch
+        w0, b0 = _ffn_in_fused(sa, sa.out_proj, x.dtype)
+        h = _Hip.layernorm_gelu(_Hip.linear_cat(x, c0, c1, w0, b0), sa.ffn[1])
+        x = _Hip.linear(h, sa.ffn[3].weight, sa.ffn[3].bias, res=x)
+        wc, bc = _cached(ca, "_qkv_stacked", (ca.to_qk.weight, ca.to_qk.bias, ca.to_v.weight, ca.to_v.bias),
+                         x.dtype, lambda: (torch.cat((ca.to_qk.weight, ca.to_v.weight), 0),
+                                           torch.cat((ca.to_qk.bias, ca.to_v.bias), 0)))
+        (qk0, qk1), (v0, v1) = _Hip.linear_split2(x, wc, bc, ca.heads, splits)
+        m0, m1 = attention([(qk0, qk1, v1), (qk1, qk0, v0)])            # cross: one launch
+        w0, b0 = _ffn_in_fused(ca, ca.to_out, x.dtype)
+        h = _Hip.layernorm_gelu(_Hip.linear_cat(x, m0, m1, w0, b0), ca.ffn[1])
+        return _Hip.linear(h, ca.ffn[3].weight, ca.ffn[3].bias, res=x)
 
 
 def log_double_softmax(sim: torch.Tensor, z0: torch.Tensor, z1: torch.Tensor) -> torch.Tensor:

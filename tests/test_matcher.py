@@ -136,6 +136,54 @@ def test_gpu_matcher_matches_reference(name, glue, dtype, tol_d, tol_s):
     assert len(got & ref) >= MATCH_RECALL * len(ref)
 
 
+def _check_fused_linear(mt, blk, dev, rnd, n0, n1, h):
+    """lg_linear* against framework GEMMs (fp32 math on the same fp16 operands), tolerances for
+    fp16 outputs of K = 256 / 512 dot products."""
+    F = torch.nn.functional
+    dt = torch.float16
+    f32 = lambda t: t.float()  # noqa: E731
+    x = rnd(1, n0 + n1, 256) * 0.5
+    tol = 2e-2
+    # plain + residual (K = 512)
+    a, res = rnd(1, n0 + n1, 512) * 0.5, rnd(1, n0 + n1, 256)
+    w, b = rnd(256, 512) * 0.05, rnd(256) * 0.1
+    ref = F.linear(f32(a), f32(w), f32(b))
+    assert float((mt._Hip.linear(a, w, b).float() - ref).abs().max()) <= tol
+    assert float((mt._Hip.linear(a, w, b, res=res).float() - (ref + f32(res))).abs().max()) <= tol
+    # [x | merged heads] gathered on load (K = 512, N = 512)
+    c0, c1 = rnd(1, h, n0, 64), rnd(1, h, n1, 64)
+    w, b = rnd(512, 512) * 0.05, rnd(512) * 0.1
+    merged = torch.cat([c[0].transpose(0, 1).reshape(c.shape[2], -1) for c in (c0, c1)], 0)[None]
+    ref = F.linear(torch.cat((f32(x), f32(merged)), -1), f32(w), f32(b))
+    assert float((mt._Hip.linear_cat(x, c0, c1, w, b).float() - ref).abs().max()) <= tol
+    # self-block projection + rotary + head split (K = 256, N = 768)
+    ang = rnd(1, n0 + n1, 32).float()
+    cos = torch.cos(ang).repeat_interleave(2, -1).to(dt).contiguous()
+    sin = torch.sin(ang).repeat_interleave(2, -1).to(dt).contiguous()
+    blk32 = mt.SelfBlock(256, h).to(dev)
+    with torch.no_grad():
+        blk16 = mt.SelfBlock(256, h).to(dev, dt)
+        blk16.load_state_dict(blk.state_dict())
+        blk32.load_state_dict(blk.state_dict())
+        ref = blk32.qkv(f32(x), f32(cos), f32(sin), (n0, n1), hip=False)
+        wq, bq = mt._qkv_perm(blk16, dt)
+        got = mt._Hip.linear_qkv_rotary(x, wq, bq, cos, sin, h, (n0, n1))
+    for r3, g3 in zip(ref, got):
+        for r_, g_ in zip(r3, g3):
+            assert float((r_ - g_.float()).abs().max()) <= tol
+    # cross-block to_qk | to_v + head split (K = 256, N = 512)
+    cb = mt.CrossBlock(256, h).to(dev)
+    with torch.no_grad():
+        wc = torch.cat((cb.to_qk.weight, cb.to_v.weight), 0).to(dt)
+        bc = torch.cat((cb.to_qk.bias, cb.to_v.bias), 0).to(dt)
+        (a0, a1), (b0, b1) = mt._Hip.linear_split2(x, wc, bc, h, (n0, n1))
+        xs = f32(x)
+        refs = cb.heads_of(F.linear(xs, f32(wc[:256]), f32(bc[:256])), (n0, n1)) + \
+            cb.heads_of(F.linear(xs, f32(wc[256:]), f32(bc[256:])), (n0, n1))
+    for r_, g_ in zip(refs, (a0, a1, b0, b1)):
+        assert float((r_ - g_.float()).abs().max()) <= tol
+
+
 # ---- the glue kernels one by one against the torch restatement (include/lightglue_glue.h) ----
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["float32", "float16"])
@@ -188,6 +236,9 @@ def test_glue_kernels_match_torch(dtype):
         ref = torch.nn.functional.gelu(ln(hx).float()).to(dt)
         tol_ln = 2e-2 if dtype == "float16" else 1e-4
         assert float((mt._Hip.layernorm_gelu(hx, ln).float() - ref.float()).abs().max()) <= tol_ln
+        if dtype == "float16":  # the fused projections (csrc/lightglue_linear.hip, fp16 only)
+            _check_fused_linear(mt, blk, dev, rnd, n0, n1, h)
+            _check_fused_linear(mt, blk, dev, rnd, 700, 1301, h)
         for m_, n_ in ((130, 211), (1024, 777), (1, 2000), (2000, 5)):  # column pass: 128-row chunks
             sim = rnd(1, m_, n_).float() * 5
             z0, z1 = rnd(1, m_, 1).float(), rnd(1, n_, 1).float()
