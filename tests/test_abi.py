@@ -231,6 +231,26 @@ def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
     assert out[2] == 1 and out[0] == 4
 
 
+@pytest.mark.parametrize("batch,nq,nkv,direct", [
+    (1, 1024, 1024, True),     # the metric call: 128 blocks of 32 rows, 1024 keys
+    (1, 2048, 1024, True),     # 256 blocks: still one residency round
+    (2, 2048, 1024, False),    # 512 blocks: the ring kernel fills the chip by itself
+    (1, 1024, 1025, False),    # more keys than 8 waves x 2 tiles
+    (1, 256, 256, True),
+    (1, 1, 1, True),
+    (8, 1024, 1024, False),    # batched: 1024 blocks
+    (2, 1024, 512, True),
+])
+def test_planner_single_pass_rule(lib, batch, nq, nkv, direct):
+    """plan code 21 (single-pass kernel) iff fp16, nkv <= 1024 and <= 256 32-row blocks; it needs
+    no workspace and never splits."""
+    out = (ctypes.c_int32 * 4)()
+    need = lib.mha_hd64_plan(batch, 4, nq, nkv, 5242880, out)
+    assert (out[0] == 21) == direct
+    if direct:
+        assert need == 0 and out[2] == 1
+
+
 def test_abort_mode_aborts_like_plugin_assert():
     """mha_hd64_set_abort_on_error(1) reproduces PLUGIN_ASSERT's abort() (checkMacrosPlugin.cpp:118-128)."""
     code = (

@@ -572,3 +572,32 @@ def test_direct_kernel_deterministic_and_capturable(dev):
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(a, b) and torch.equal(out, a)
+
+
+def test_planner_default_random_shapes(dev, oracle_mod):
+    """Seeded random shapes through the planner's default plan (single-pass kernel or LDS ring,
+    split or not) for both output types, against the C oracle on sampled rows."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    rng = np.random.default_rng(2024)
+    ws = torch.empty(5242880, dtype=torch.uint8, device=dev)
+    for case in range(12):
+        batch = int(rng.integers(1, 3))
+        nq = int(rng.integers(1, 2049))
+        nkv = int(rng.integers(1, 2049))
+        qn, kn, vn = synth.qkv(900 + case, nq, nkv, batch=batch)
+        q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
+        rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 24)), nq - 1])
+        ref = oracle_mod.attention_c(np.ascontiguousarray(q16[:, :, rows]), k16, v16)
+        q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+        for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
+            o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
+            st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), batch, 4, nq, nkv,
+                                            0, int(out_dt == torch.float32), 0, 0, 0, ws.data_ptr(), ws.numel(),
+                                            torch.cuda.current_stream().cuda_stream, 3)
+            assert st == 0, _lib.last_error()
+            torch.cuda.synchronize()
+            got = o.float().cpu().numpy()
+            assert np.isfinite(got).all(), (batch, nq, nkv)
+            assert _maxdiff(got[:, :, rows], ref) <= tol, (batch, nq, nkv, out_dt)
