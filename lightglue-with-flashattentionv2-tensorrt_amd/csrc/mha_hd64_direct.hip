@@ -25,6 +25,7 @@
 // at most 256 such workgroups (one residency round); everything else runs the ring kernel.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "mha_hd64_device.h"
@@ -49,10 +50,21 @@
 namespace mha_hd64 {
 namespace {
 
-template <typename TOut, int TPW, bool MULTI>
-__global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
-    // (16 waves x 1 tile, four per SIMD, measured 7.7 us against 6.3 us for 8 x 2 at 1x4x1024x1024)
-    constexpr int KW = 8;                               // waves (key slices) per workgroup
+// s_waitcnt vmcnt(N) for a compile-time N (multiples of 8 up to 24)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N % 8 == 0 && N <= 24, "vmcnt");
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+}
+
+// KW waves (key slices) per workgroup x TPW 64-key tiles per wave. (16 waves x 1 tile, four per
+// SIMD, measured 7.7 us against 6.3 us for 8 x 2 at 1x4x1024x1024.)
+template <typename TOut, int KW, int TPW, bool MULTI>
+__global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) {
+    constexpr int NT = 64 * KW;
     constexpr int BLOCK_M = 32;                         // query rows per workgroup
     constexpr int WAVE_KEYS = kTileKV * TPW;            // keys per wave
     constexpr int OROW = 68;                            // epilogue fp32 row pitch (64 dims + 4 pad)
@@ -157,10 +169,9 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
         }
         dma_rows(k_rs, true);
         // Q and K(0) have landed (issue order: Q, K(0) 8 pieces, K(1) 8 pieces)
-        if constexpr (TPW == 2)
-            asm volatile("s_waitcnt vmcnt(8)" : "+v"(qraw[0]), "+v"(qraw[1]), "+v"(qraw[2]), "+v"(qraw[3])::"memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(qraw[0]), "+v"(qraw[1]), "+v"(qraw[2]), "+v"(qraw[3])::"memory");
+        // Q and K(0) have landed (issue order: Q, then K(0) .. K(TPW-1), 8 pieces each)
+        wait_vm<8 * (TPW - 1)>();
+        asm volatile("" : "+v"(qraw[0]), "+v"(qraw[1]), "+v"(qraw[2]), "+v"(qraw[3])::"memory");
         DSTAMP(1);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
@@ -191,10 +202,27 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
         // tile runs, even one wholly past nkv (its keys are masked: P = 0 and the max does not
         // move), so no branch separates the up-front loads from their uses.
         f16x8 p[TPW][2][2];  // P (fp16) as the B operand: p[t][half][k-step]
+        f32x16 sc[TPW][2];   // scores of tiles 1.. (log2 units, against the first tile's max)
+        auto exp_pack = [&](f32x16 c0, f32x16 c1, f16x8(&pt)[2][2]) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                if (MHA_ABL & ABL_NO_EXP) continue;
+                c0[e] = __builtin_amdgcn_exp2f(c0[e]);
+                c1[e] = __builtin_amdgcn_exp2f(c1[e]);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                pt[0][0][e] = (f16)c0[e];
+                pt[0][1][e] = (f16)c0[8 + e];
+                pt[1][0][e] = (f16)c1[e];
+                pt[1][1][e] = (f16)c1[8 + e];
+            }
+        };
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
             f16x8 kf[8];
-            if (t > 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // K(t) landed; V(t-1) may not have
+            // K(t) landed: younger are K(t+1..) and V(0..t-1), 8 pieces each
+            if (t > 0) wait_vm<8 * (TPW - 1)>();
             read_k(t, kf);
             // K(t)'s fragments are in registers before V(t)'s DMA overwrites slot t
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]), "+v"(kf[4]),
@@ -232,21 +260,10 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
             };
             if (bias_last) chain(std::false_type{});
             else chain(std::true_type{});
-            const float mx = xhalf_max(tree_max(c0, c1));
-            // online softmax: the first tile sets the max; a later one moves it only when a query's
-            // tile max exceeds it by > kRescaleThr (wave-uniform branch). No PV has run yet, so a
-            // move rescales the earlier tiles' probabilities instead of O.
-            if (t == 0 || __builtin_amdgcn_ballot_w64(mx > kRescaleThr) != 0) {
-                const float d = t == 0 ? ((mx < kEmptyMax) ? 0.f : mx) : fmaxf(mx, 0.f);
-                if (t > 0) {
-                    const f16 alpha = (f16)__builtin_amdgcn_exp2f(-d);
-#pragma unroll
-                    for (int t2 = 0; t2 < t; ++t2)
-#pragma unroll
-                        for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-                            for (int ss = 0; ss < 2; ++ss) p[t2][h2][ss] *= alpha;
-                }
+            if (t == 0) {
+                // the first tile sets the running max (a fully masked tile: m = 0)
+                const float mx = xhalf_max(tree_max(c0, c1));
+                const float d = (mx < kEmptyMax) ? 0.f : mx;
                 m_run += d;
                 set_bias();
                 if (bias_last) {
@@ -256,28 +273,49 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
                     c0 -= d;
                     c1 -= d;
                 }
+                exp_pack(c0, c1, p[0]);
+            } else {
+                sc[t][0] = c0;
+                sc[t][1] = c1;
+            }
+        }
+        // Later tiles' scores were taken against the first tile's max: ONE decision for all of them
+        // (wave-uniform, rare) moves the max by the largest excess over kRescaleThr, rescaling the
+        // first tile's probabilities and the later scores; then their exponentials. No branch sits
+        // between the tiles, so their MFMAs interleave with the first tile's exponentials.
+        if constexpr (TPW > 1) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int t = 1; t < TPW; ++t) mx = fmaxf(mx, tree_max(sc[t][0], sc[t][1]));
+            mx = xhalf_max(mx);
+            if (__builtin_amdgcn_ballot_w64(mx > kRescaleThr) != 0) {
+                const float d = fmaxf(mx, 0.f);
+                const f16 alpha = (f16)__builtin_amdgcn_exp2f(-d);
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+                    for (int ss = 0; ss < 2; ++ss) p[0][h2][ss] *= alpha;
+#pragma unroll
+                for (int t = 1; t < TPW; ++t) {
+                    sc[t][0] -= d;
+                    sc[t][1] -= d;
+                }
+                m_run += d;
             }
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                if (MHA_ABL & ABL_NO_EXP) continue;
-                c0[e] = __builtin_amdgcn_exp2f(c0[e]);
-                c1[e] = __builtin_amdgcn_exp2f(c1[e]);
-            }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                p[t][0][0][e] = (f16)c0[e];
-                p[t][0][1][e] = (f16)c0[8 + e];
-                p[t][1][0][e] = (f16)c1[e];
-                p[t][1][1][e] = (f16)c1[8 + e];
-            }
+            for (int t = 1; t < TPW; ++t) exp_pack(sc[t][0], sc[t][1], p[t]);
         }
         DSTAMP(2);
         // Phase 2: V in LDS -> Oᵀ = Vᵀ·Pᵀ and the row sums.
 #pragma unroll
         for (int t = 0; t < TPW; ++t) {
             // V(t) landed (V(t+1)'s 8 pieces may still be in flight)
-            if (t + 1 < TPW) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            switch (TPW - 1 - t) {  // V(t) landed (V(t+1..) may still be in flight)
+                case 0: wait_vm<0>(); break;
+                case 1: wait_vm<8>(); break;
+                case 2: wait_vm<16>(); break;
+                default: wait_vm<24>(); break;
+            }
             if (t == 0) DSTAMP(3);
             const unsigned va0 = region + t * kTileBytes + v_lane + 64 * vb;
             const unsigned va1 = region + t * kTileBytes + v_lane + 64 * (1 - vb);
@@ -323,8 +361,11 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
     }
     __syncthreads();
     DSTAMP(5);
-    // thread -> (row, 4 dims): 32 rows x 16 chunks = 512 items
-    const int row = tid >> 4, c = (tid & 15) * 4;
+    // thread -> (row, 4 dims): 32 rows x 16 chunks = 512 items (two per thread at 4 waves)
+#pragma unroll
+    for (int pass = 0; pass < 512 / NT; ++pass) {
+    const int idx = pass * NT + tid;
+    const int row = idx >> 4, c = (idx & 15) * 4;
     const int q = qtile * BLOCK_M + row;
     float2 ml[KW];
     float M = -INFINITY;
@@ -346,29 +387,40 @@ __global__ __launch_bounds__(512, 1) void mha_hd64_direct_kernel(FwdArgs a) {
                                                       (unsigned)(nq * kHeadDim * sizeof(TOut)));
         store4b<TOut, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)), acc * (1.f / L));
     }
+    }
 #ifdef MHA_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     DSTAMP(6);
 #endif
 }
 
-template <typename TOut, int TPW>
+template <typename TOut, int KW, int TPW>
 hipError_t launch_direct_t(const FwdArgs& a, int grid, hipStream_t stream) {
     if (a.n_calls > 1)
-        hipLaunchKernelGGL((mha_hd64_direct_kernel<TOut, TPW, true>), dim3(grid), dim3(512), 0, stream, a);
+        hipLaunchKernelGGL((mha_hd64_direct_kernel<TOut, KW, TPW, true>), dim3(grid), dim3(64 * KW), 0, stream, a);
     else
-        hipLaunchKernelGGL((mha_hd64_direct_kernel<TOut, TPW, false>), dim3(grid), dim3(512), 0, stream, a);
+        hipLaunchKernelGGL((mha_hd64_direct_kernel<TOut, KW, TPW, false>), dim3(grid), dim3(64 * KW), 0, stream, a);
     return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t launch_direct(const FwdArgs& a, int grid, int tiles_per_wave, bool out_f32, hipStream_t stream) {
-    switch (tiles_per_wave * 2 + (out_f32 ? 1 : 0)) {
-        case 2: return launch_direct_t<f16, 1>(a, grid, stream);
-        case 3: return launch_direct_t<float, 1>(a, grid, stream);
-        case 4: return launch_direct_t<f16, 2>(a, grid, stream);
-        case 5: return launch_direct_t<float, 2>(a, grid, stream);
+    // 4 waves x twice the tiles (one wave per SIMD): 6.02 vs 6.16 us at 1x4x1024^2, 4.33 vs 4.95 at
+    // 512^2 against 8 waves; MHA_HD64_DIRECT_WAVES=8 selects the 8-wave form (comparison hook)
+    static const bool four = [] {
+        const char* e = std::getenv("MHA_HD64_DIRECT_WAVES");
+        return !(e && e[0] == '8');
+    }();
+    switch ((four ? 100 : 0) + tiles_per_wave * 2 + (out_f32 ? 1 : 0)) {
+        case 2: return launch_direct_t<f16, 8, 1>(a, grid, stream);
+        case 3: return launch_direct_t<float, 8, 1>(a, grid, stream);
+        case 4: return launch_direct_t<f16, 8, 2>(a, grid, stream);
+        case 5: return launch_direct_t<float, 8, 2>(a, grid, stream);
+        case 102: return launch_direct_t<f16, 4, 2>(a, grid, stream);
+        case 103: return launch_direct_t<float, 4, 2>(a, grid, stream);
+        case 104: return launch_direct_t<f16, 4, 4>(a, grid, stream);
+        case 105: return launch_direct_t<float, 4, 4>(a, grid, stream);
         default: return hipErrorInvalidValue;
     }
 }
