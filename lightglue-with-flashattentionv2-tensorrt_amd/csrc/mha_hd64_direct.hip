@@ -138,9 +138,9 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * i),
                                                      16, voff, 1024 * i, 0, 0);
         };
-        auto dma_rows = [&](__amdgpu_buffer_rsrc_t rs, bool is_k) {  // all of the wave's K
+        auto dma_k = [&](int t0, int t1) {  // K of tiles [t0, t1) into their slots
 #pragma unroll
-            for (int i = 0; i < 8 * TPW; ++i) dma_piece(rs, is_k ? k_lane[i & 1] : v_lane_off, i);
+            for (int i = 8 * t0; i < 8 * t1; ++i) dma_piece(k_rs, k_lane[i & 1], i);
         };
         auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, int t) {  // V of tile t into slot t
 #pragma unroll
@@ -167,12 +167,15 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
                               : "=v"(qraw[s])
                               : "v"((unsigned)(q_row * kHeadDim + 16 * s + 8 * hh) * 2), "s"(q_rs));
         }
-        dma_rows(k_rs, true);
-        // Q and K(0) have landed (issue order: Q, K(0) 8 pieces, K(1) 8 pieces)
-        // Q and K(0) have landed (issue order: Q, then K(0) .. K(TPW-1), 8 pieces each)
-        wait_vm<8 * (TPW - 1)>();
+        // K(0) and K(1) first: the first tile's K is not queued behind the whole wave's K
+        constexpr int KFIRST = TPW < 2 ? TPW : 2;
+        dma_k(0, KFIRST);
+        // Q and K(0) have landed (issue order: Q, K(0), K(1), 8 pieces per tile)
+        wait_vm<8 * (KFIRST - 1)>();
         asm volatile("" : "+v"(qraw[0]), "+v"(qraw[1]), "+v"(qraw[2]), "+v"(qraw[3])::"memory");
         DSTAMP(1);
+        // the rest of K; every later K(t) wait sees K(t+1..) and V(0..t-1) younger: vmcnt(8*(TPW-1))
+        dma_k(KFIRST, TPW);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -203,6 +206,41 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         // move), so no branch separates the up-front loads from their uses.
         f16x8 p[TPW][2][2];  // P (fp16) as the B operand: p[t][half][k-step]
         f32x16 sc[TPW][2];   // scores of tiles 1.. (log2 units, against the first tile's max)
+        // Oᵀ += Vᵀ·Pᵀ for tile t and the row sums, once V(t) has landed (V(t+1..) may be in flight)
+        auto pv = [&](int t) {
+            switch (TPW - 1 - t) {
+                case 0: wait_vm<0>(); break;
+                case 1: wait_vm<8>(); break;
+                case 2: wait_vm<16>(); break;
+                default: wait_vm<24>(); break;
+            }
+            if (t == 0) DSTAMP(3);
+            const unsigned va0 = region + t * kTileBytes + v_lane + 64 * vb;
+            const unsigned va1 = region + t * kTileBytes + v_lane + 64 * (1 - vb);
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    const unsigned rowc = 128 * (32 * jj + 16 * ss);
+                    const f16x8 vfa = cat8(tr_read(lds, va0 + rowc), tr_read(lds, va0 + rowc + 8 * 128));
+                    const f16x8 vfb = cat8(tr_read(lds, va1 + rowc), tr_read(lds, va1 + rowc + 8 * 128));
+                    if (MHA_ABL & ABL_NO_PV) {
+                        keep_live(vfa);
+                        keep_live(vfb);
+                        keep_live(p[t][jj][ss]);
+                        if (t == 0 && jj == 0 && ss == 0) {
+                            o0 = o1 = f32x16{};
+                            l_acc = f32x4{0.f, 0.f, 0.f, 0.f};
+                        }
+                        continue;
+                    }
+                    const bool first = t == 0 && jj == 0 && ss == 0;  // accumulators start at inline 0
+                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa, p[t][jj][ss], first ? f32x16{} : o0, 0, 0, 0);
+                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb, p[t][jj][ss], first ? f32x16{} : o1, 0, 0, 0);
+                    l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, p[t][jj][ss], first ? f32x4{} : l_acc, 0,
+                                                                   0, 0);
+                }
+        };
         auto exp_pack = [&](f32x16 c0, f32x16 c1, f16x8(&pt)[2][2]) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
@@ -281,20 +319,20 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         }
         // Later tiles' scores were taken against the first tile's max: ONE decision for all of them
         // (wave-uniform, rare) moves the max by the largest excess over kRescaleThr, rescaling the
-        // first tile's probabilities and the later scores; then their exponentials. No branch sits
+        // first tile's O and row sums and the later scores; then their exponentials. No branch sits
         // between the tiles, so their MFMAs interleave with the first tile's exponentials.
         if constexpr (TPW > 1) {
+            pv(0);  // tile 0's PV on the matrix pipe beside the later tiles' max trees and exponentials
             float mx = -INFINITY;
 #pragma unroll
             for (int t = 1; t < TPW; ++t) mx = fmaxf(mx, tree_max(sc[t][0], sc[t][1]));
             mx = xhalf_max(mx);
             if (__builtin_amdgcn_ballot_w64(mx > kRescaleThr) != 0) {
                 const float d = fmaxf(mx, 0.f);
-                const f16 alpha = (f16)__builtin_amdgcn_exp2f(-d);
-#pragma unroll
-                for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-                    for (int ss = 0; ss < 2; ++ss) p[0][h2][ss] *= alpha;
+                const float alpha = __builtin_amdgcn_exp2f(-d);
+                o0 *= alpha;  // tile 0 is already in O and its row sums
+                o1 *= alpha;
+                l_acc *= alpha;
 #pragma unroll
                 for (int t = 1; t < TPW; ++t) {
                     sc[t][0] -= d;
@@ -306,39 +344,9 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
             for (int t = 1; t < TPW; ++t) exp_pack(sc[t][0], sc[t][1], p[t]);
         }
         DSTAMP(2);
-        // Phase 2: V in LDS -> Oᵀ = Vᵀ·Pᵀ and the row sums.
+        // Phase 2: the remaining tiles' Oᵀ += Vᵀ·Pᵀ (tile 0's ran before the decision above).
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) {
-            // V(t) landed (V(t+1)'s 8 pieces may still be in flight)
-            switch (TPW - 1 - t) {  // V(t) landed (V(t+1..) may still be in flight)
-                case 0: wait_vm<0>(); break;
-                case 1: wait_vm<8>(); break;
-                case 2: wait_vm<16>(); break;
-                default: wait_vm<24>(); break;
-            }
-            if (t == 0) DSTAMP(3);
-            const unsigned va0 = region + t * kTileBytes + v_lane + 64 * vb;
-            const unsigned va1 = region + t * kTileBytes + v_lane + 64 * (1 - vb);
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-                for (int ss = 0; ss < 2; ++ss) {
-                    const unsigned rowc = 128 * (32 * jj + 16 * ss);
-                    const f16x8 vfa = cat8(tr_read(lds, va0 + rowc), tr_read(lds, va0 + rowc + 8 * 128));
-                    const f16x8 vfb = cat8(tr_read(lds, va1 + rowc), tr_read(lds, va1 + rowc + 8 * 128));
-                    if (MHA_ABL & ABL_NO_PV) {
-                        keep_live(vfa);
-                        keep_live(vfb);
-                        keep_live(p[t][jj][ss]);
-                        continue;
-                    }
-                    const bool first = t == 0 && jj == 0 && ss == 0;  // accumulators start at inline 0
-                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa, p[t][jj][ss], first ? f32x16{} : o0, 0, 0, 0);
-                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb, p[t][jj][ss], first ? f32x16{} : o1, 0, 0, 0);
-                    l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, p[t][jj][ss], first ? f32x4{} : l_acc, 0,
-                                                                   0, 0);
-                }
-        }
+        for (int t = (TPW > 1 ? 1 : 0); t < TPW; ++t) pv(t);
     }
 
     DSTAMP(4);
