@@ -369,11 +369,11 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
     }
     __syncthreads();
     DSTAMP(5);
-    // thread -> (row, 4 dims): 32 rows x 16 chunks = 512 items (two per thread at 4 waves)
-#pragma unroll
-    for (int pass = 0; pass < 512 / NT; ++pass) {
-    const int idx = pass * NT + tid;
-    const int row = idx >> 4, c = (idx & 15) * 4;
+    // thread -> (row, DPT dims): 32 rows x 64/DPT chunks, one item per thread (DPT = 8 at 4 waves:
+    // one 16-B fp16 store; DPT = 4 at 8 waves)
+    constexpr int DPT = 32 * kHeadDim / NT;
+    static_assert(DPT == 4 || DPT == 8, "epilogue items");
+    const int row = tid / (kHeadDim / DPT), c = (tid % (kHeadDim / DPT)) * DPT;
     const int q = qtile * BLOCK_M + row;
     float2 ml[KW];
     float M = -INFINITY;
@@ -382,19 +382,21 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         ml[k] = *reinterpret_cast<const float2*>(mlb + (k * BLOCK_M + row) * 2);
         M = fmaxf(M, ml[k].x);
     }
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     float L = 0.f;
 #pragma unroll
     for (int k = 0; k < KW; ++k) {
         const float w = (ml[k].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[k].x - M);
         L += w * ml[k].y;
-        acc += w * *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(smem + k * RS) + row * OROW + c);
+        const float* src = reinterpret_cast<const float*>(smem + k * RS) + row * OROW + c;
+        acc0 += w * *reinterpret_cast<const f32x4*>(src);
+        if constexpr (DPT == 8) acc1 += w * *reinterpret_cast<const f32x4*>(src + 4);
     }
     if (q < nq && !(MHA_ABL & ABL_NO_STORE)) {
         const __amdgpu_buffer_rsrc_t o_rs = make_rsrc(reinterpret_cast<TOut*>(ca.o) + (size_t)bh * nq * kHeadDim,
                                                       (unsigned)(nq * kHeadDim * sizeof(TOut)));
-        store4b<TOut, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)), acc * (1.f / L));
-    }
+        const float inv = 1.f / L;
+        store_dims<TOut, DPT, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)), acc0 * inv, acc1 * inv);
     }
 #ifdef MHA_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
