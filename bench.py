@@ -491,8 +491,8 @@ def main():
         t_call = statistics.median(event_durations_ms(torch, full_call, 200, stream)[20:])
         achieved = flops / (t_main * 1e-3) / 1e12
         traffic = load_traffic("direct_kernel_bytes_per_launch" if direct else "main_kernel_bytes_per_launch")
-        kname = ("mha_hd64_direct_kernel<f16,TPW=2> (single pass: 32 query rows x all keys per workgroup, "
-                 "no split)" if direct else
+        kname = ("mha_hd64_direct_kernel<f16,4 waves,4 tiles> (single pass: 32 query rows x all 1024 keys per "
+                 "workgroup, no split)" if direct else
                  f"mha_hd64_fwd_kernel<f16,f16,{q_waves},{kv_waves}> ({splits}-way KV split, in-launch combine)")
         result["roofline"] = {
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
