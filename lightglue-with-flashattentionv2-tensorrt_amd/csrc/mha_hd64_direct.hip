@@ -207,8 +207,8 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         f16x8 p[TPW][2][2];  // P (fp16) as the B operand: p[t][half][k-step]
         f32x16 sc[TPW][2];   // scores of tiles 1.. (log2 units, against the first tile's max)
         // Oᵀ += Vᵀ·Pᵀ for tile t and the row sums, once V(t) has landed (V(t+1..) may be in flight)
-        auto pv = [&](int t) {
-            switch (TPW - 1 - t) {
+        auto pv = [&](int t, bool waited = false) {
+            if (!waited) switch (TPW - 1 - t) {
                 case 0: wait_vm<0>(); break;
                 case 1: wait_vm<8>(); break;
                 case 2: wait_vm<16>(); break;
@@ -319,20 +319,20 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         }
         // Later tiles' scores were taken against the first tile's max: ONE decision for all of them
         // (wave-uniform, rare) moves the max by the largest excess over kRescaleThr, rescaling the
-        // first tile's O and row sums and the later scores; then their exponentials. No branch sits
+        // first tile's probabilities and the later scores; then their exponentials. No branch sits
         // between the tiles, so their MFMAs interleave with the first tile's exponentials.
         if constexpr (TPW > 1) {
-            pv(0);  // tile 0's PV on the matrix pipe beside the later tiles' max trees and exponentials
             float mx = -INFINITY;
 #pragma unroll
             for (int t = 1; t < TPW; ++t) mx = fmaxf(mx, tree_max(sc[t][0], sc[t][1]));
             mx = xhalf_max(mx);
             if (__builtin_amdgcn_ballot_w64(mx > kRescaleThr) != 0) {
                 const float d = fmaxf(mx, 0.f);
-                const float alpha = __builtin_amdgcn_exp2f(-d);
-                o0 *= alpha;  // tile 0 is already in O and its row sums
-                o1 *= alpha;
-                l_acc *= alpha;
+                const f16 alpha = (f16)__builtin_amdgcn_exp2f(-d);
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+                    for (int ss = 0; ss < 2; ++ss) p[0][h2][ss] *= alpha;
 #pragma unroll
                 for (int t = 1; t < TPW; ++t) {
                     sc[t][0] -= d;
@@ -340,13 +340,16 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
                 }
                 m_run += d;
             }
+            pv(0);  // tile 0's PV on the matrix pipe beside the later tiles' exponentials (one block)
 #pragma unroll
             for (int t = 1; t < TPW; ++t) exp_pack(sc[t][0], sc[t][1], p[t]);
         }
         DSTAMP(2);
-        // Phase 2: the remaining tiles' Oᵀ += Vᵀ·Pᵀ (tile 0's ran before the decision above).
+        // Phase 2: the remaining tiles' Oᵀ += Vᵀ·Pᵀ (tile 0's ran beside the exponentials). Every V
+        // has long landed by now: one wait, so the compiler may hoist later tiles' fragment reads.
+        if constexpr (TPW > 1) wait_vm<0>();
 #pragma unroll
-        for (int t = (TPW > 1 ? 1 : 0); t < TPW; ++t) pv(t);
+        for (int t = (TPW > 1 ? 1 : 0); t < TPW; ++t) pv(t, TPW > 1);
     }
 
     DSTAMP(4);
