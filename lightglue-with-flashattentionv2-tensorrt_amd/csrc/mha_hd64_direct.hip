@@ -176,10 +176,23 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         DSTAMP(1);
         // the rest of K; every later K(t) wait sees K(t+1..) and V(0..t-1) younger: vmcnt(8*(TPW-1))
         dma_k(KFIRST, TPW);
+        // q * 0.125·log2(e) in fp32, rounded to fp16: one v_fma_mix{lo,hi}_f16 per value (the compiler
+        // emits convert + multiply + pack, twice the vector instructions)
+        {
+            const float sc = kScaleLog2;
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+            for (int s = 0; s < 4; ++s) {
+                const u32x4 in = __builtin_bit_cast(u32x4, qraw[s]);
+                u32x4 outv;
 #pragma unroll
-            for (int e = 0; e < 8; ++e) qf[s][e] = (f16)((float)qraw[s][e] * kScaleLog2);
+                for (int w = 0; w < 4; ++w)
+                    asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[1,0,0]\n\t"
+                        "v_fma_mixhi_f16 %0, %1, %2, 0 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                        : "=&v"(outv[w])
+                        : "v"(in[w]), "v"(sc));
+                qf[s] = __builtin_bit_cast(f16x8, outv);
+            }
+        }
 
         // Row sums on the matrix pipe and the bias k-step: as the ring kernel (mha_hd64_kernels.hip).
         const f16 sel = (((lane & 15) >> 2) & 1) == ((lane >> 4) & 1) ? (f16)1.f : (f16)0.f;
