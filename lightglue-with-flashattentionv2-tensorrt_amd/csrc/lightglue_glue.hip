@@ -156,6 +156,41 @@ __global__ __launch_bounds__(256) void ln_gelu_kernel(const T* __restrict__ x, c
     }
 }
 
+// fp16, dim 512 (the matcher's FFN width): a lane owns 8 contiguous columns (one 16-B load of x,
+// gamma and beta), sum and sum of squares reduced together (fp32, E[x^2] - mean^2).
+__global__ __launch_bounds__(256) void ln_gelu_512_f16_kernel(const f16* __restrict__ x, const f16* __restrict__ g,
+                                                              const f16* __restrict__ bta, int rows, float eps,
+                                                              f16* y) {
+    typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const f16x8 xv = *reinterpret_cast<const f16x8*>(x + (size_t)row * 512 + lane * 8);
+    const f16x8 gv = *reinterpret_cast<const f16x8*>(g + lane * 8);
+    const f16x8 bv = *reinterpret_cast<const f16x8*>(bta + lane * 8);
+    float v[8], s = 0.f, q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        v[e] = (float)xv[e];
+        s += v[e];
+        q += v[e] * v[e];
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {  // two independent shuffle chains
+        s += __shfl_xor(s, m, 64);
+        q += __shfl_xor(q, m, 64);
+    }
+    const float mean = s * (1.f / 512);
+    const float rstd = rsqrtf(fmaxf(q * (1.f / 512) - mean * mean, 0.f) + eps);
+    f16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float t = (v[e] - mean) * rstd * (float)gv[e] + (float)bv[e];
+        o[e] = (f16)(0.5f * t * (1.f + erff(t * 0.70710678118654752f)));
+    }
+    *reinterpret_cast<f16x8*>(y + (size_t)row * 512 + lane * 8) = o;
+}
+
 // ---- dual log-softmax ----
 // Pass 1 (lse_kernel): blocks [0, rb) -> row logsumexp (one wave per row); blocks [rb, ...) ->
 // column partials: a block is 64 consecutive columns x one chunk of kColChunk rows, its 256
@@ -338,6 +373,13 @@ int32_t lg_layernorm_gelu(int32_t dtype, const void* x, const void* gamma, const
         return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_layernorm_gelu", "bad arguments");
     if (rows == 0) return MHA_HD64_STATUS_SUCCESS;
     const dim3 grid((rows + 3) / 4);
+    if (dtype == MHA_HD64_DT_HALF && dim == 512 &&
+        ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
+          reinterpret_cast<uintptr_t>(y)) & 15) == 0) {
+        hipLaunchKernelGGL(ln_gelu_512_f16_kernel, grid, dim3(256), 0, stream, (const f16*)x, (const f16*)gamma,
+                           (const f16*)beta, rows, eps, (f16*)y);
+        return launched("lg_layernorm_gelu");
+    }
 #define LG_LN(PER)                                                                                              \
     case PER:                                                                                                   \
         if (dtype == MHA_HD64_DT_HALF)                                                                          \
