@@ -242,8 +242,8 @@ def sweep(torch, lib, device, stream, nq, nkv):
         qn, kn, vn = synth.qkv(7, nq, nkv, batch=batch)
         q, k, v = (torch.from_numpy(x).to(device).half().contiguous() for x in (qn, kn, vn))
         o = torch.empty_like(q)
-        for qw, kw in ((4, 1), (2, 2), (1, 2), (4, 2), (2, 4), (1, 8), (21, 0)):
-            for splits in ((0,) if qw == 21 or kw >= 4 else (1, 2, 4, 8, 16)):
+        for qw, kw in ((4, 1), (2, 2), (1, 2), (4, 2), (2, 4), (1, 8), (21, 0), (22, 0)):
+            for splits in ((0,) if qw >= 21 or kw >= 4 else (1, 2, 4, 8, 16)):
                 def run(mask=3):
                     return lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), batch,
                                                       4, nq, nkv, 0, 0, qw, kw, splits, ws_buf.data_ptr(),
@@ -471,8 +471,17 @@ def main():
         # dispatch-to-dispatch interval, an upper bound on the kernel's own duration). The production
         # form is ONE launch (split partials merged by each query group's last-arriving workgroup);
         # the two-kernel form (main + combine kernel) is timed beside it.
-        direct = q_waves == 21  # the single-pass kernel (csrc/mha_hd64_direct.hip)
+        # the single-pass kernels: 22 = 16-row blocks (csrc/mha_hd64_direct16.hip), 21 = 32-row
+        # blocks (csrc/mha_hd64_direct.hip)
+        direct = q_waves in (21, 22)
         t_main = graph_per_launch_ms(torch, lambda: forced(3), stream)
+
+        def direct32(mask):
+            lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), 1, 4, nq, nkv, 0,
+                                       0, 21, 0, 0, ws_buf.data_ptr(), ws_buf.numel(),
+                                       torch.cuda.current_stream(device).cuda_stream, mask)
+
+        t_direct32 = graph_per_launch_ms(torch, lambda: direct32(3), stream) if q_waves == 22 else None
 
         # The ring kernel's split plan for the same call, timed beside the production kernel: (1,8)
         # with the 2-way split merged in-launch, and its two-kernel form (main + combine kernel).
@@ -490,15 +499,19 @@ def main():
         lib.mha_hd64_set_fused_combine(1)
         t_call = statistics.median(event_durations_ms(torch, full_call, 200, stream)[20:])
         achieved = flops / (t_main * 1e-3) / 1e12
-        traffic = load_traffic("direct_kernel_bytes_per_launch" if direct else "main_kernel_bytes_per_launch")
-        kname = ("mha_hd64_direct_kernel<f16,4 waves,4 tiles> (single pass: 32 query rows x all 1024 keys per "
-                 "workgroup, no split)" if direct else
-                 f"mha_hd64_fwd_kernel<f16,f16,{q_waves},{kv_waves}> ({splits}-way KV split, in-launch combine)")
+        traffic = load_traffic({22: "direct16_kernel_bytes_per_launch", 21: "direct_kernel_bytes_per_launch"}.get(
+            q_waves, "main_kernel_bytes_per_launch"))
+        kname = {22: "mha_hd64_direct16_kernel<f16,4 waves,4 tiles> (single pass: 16 query rows x all 1024 keys "
+                     "per workgroup, no split)",
+                 21: "mha_hd64_direct_kernel<f16,4 waves,4 tiles> (single pass: 32 query rows x all 1024 keys per "
+                     "workgroup, no split)"}.get(
+            q_waves, f"mha_hd64_fwd_kernel<f16,f16,{q_waves},{kv_waves}> ({splits}-way KV split, in-launch combine)")
         result["roofline"] = {
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": traffic,
             "kernel": kname,
             "kernel_us": round(t_main * 1e3, 3),
+            "direct32_kernel_us": None if t_direct32 is None else round(t_direct32 * 1e3, 3),
             "ring_split_plan_us": {"in_launch_combine": round(t_ring * 1e3, 3), "main": round(t_main2 * 1e3, 3),
                                    "combine": round(t_comb2 * 1e3, 3), "two_kernels": round(t_two * 1e3, 3)},
             "timing": "graph replay of 200 back-to-back launches per kernel on the launch stream",

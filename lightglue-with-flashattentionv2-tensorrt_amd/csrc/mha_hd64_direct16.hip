@@ -1,0 +1,326 @@
+// mha_hd64_direct16.hip — single-pass FlashAttention forward, head_dim = 64, 16-row query blocks,
+// for gfx950 (MI355X).
+//
+// The operator of mha_hd64_kernels.hip / mha_hd64_direct.hip (O = softmax(Q·Kᵀ·0.125)·V per
+// (batch, head); the reference's attention_headdim_64_fp16in_fp16out.cu:253-733 /
+// …fp16in_fp32out.cu:253-703) for launches whose 32-row blocks fill at most half the chip: the
+// plugin's single 1x4x1024x1024 call is 128 blocks of 32 rows (128 of 256 CUs busy, the other
+// half idle) but 256 blocks of 16 rows. Each workgroup streams all of its head's keys as the
+// 32-row kernel does (the per-CU load volume is the same; twice the L2 reads in total), and
+// each wave does half the arithmetic.
+//  * 4 waves, wave w owns keys [64·TPW·w, 64·TPW·(w+1)); K and V by LDS-DMA into the wave's own
+//    slots (K(t) into slot t, V(t) over it once K(t)'s fragments are in registers), no barrier
+//    before the epilogue — the 32-row kernel's load schedule.
+//  * Sᵀ = K·Qᵀ on v_mfma_f32_16x16x32_f16: per 64-key tile 4 key blocks x 2 dim steps. A lane
+//    holds keys 16kb + 4g + j (j < 4) of query i = lane % 16 (g = lane / 16), so the fp16 P of
+//    key blocks 2u and 2u+1 concatenated is directly the B operand of step u of Oᵀ = Vᵀ·Pᵀ (key
+//    order k = 8g + j <-> 32u + 4g + j, 8g + 4 + j <-> 32u + 16 + 4g + j), and the matching A
+//    operand (Vᵀ) is two ds_read_b64_tr_b16 of 4 rows each (rows 4g..4g+3 and 16 + 4g..).
+//  * Softmax as the 32-row kernel: the first tile sets the running max, the later tiles' scores
+//    wait for ONE lazy-rescale decision (threshold 8, log2 units), row sums on the matrix pipe
+//    (an all-ones A operand), masking of keys past nkv on the vector pipe (partial tiles only).
+//  * Epilogue: each wave stages Oᵀ (fp32) and (m, l) in its region; one barrier; 256 threads
+//    merge (row, 4 dims) over the 4 waves and store O.
+// LDS images (bank rule of cdna_hip_programming.md §2): K rows XOR chunk (row>>1)&7 (k_off: the
+// 16 rows of every ds_read_b128 lane group on distinct 16-B slots); V rows XOR chunk
+// 2·((row>>1)&3) (the 8 rows x 2 chunks of every tr_b16 half-wave on distinct slots).
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "mha_hd64_device.h"
+#include "mha_hd64_internal.h"
+
+namespace mha_hd64 {
+namespace {
+
+template <int N>
+__device__ __forceinline__ void wait_vmc() {
+    static_assert(N % 8 == 0 && N <= 24, "vmcnt");
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+}
+
+// max over the lanes of one query (i, i+16, i+32, i+48): v_permlane32_swap then v_permlane16_swap
+__device__ __forceinline__ float xquad_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    const float y = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(y), __float_as_uint(y), false, false);
+    return fmaxf(__uint_as_float(s[0]), __uint_as_float(s[1]));
+}
+
+__device__ __forceinline__ float max16(const f32x4 (&c)[4]) {
+    float t[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) t[kb] = fmaxf(fmaxf(c[kb][0], c[kb][1]), fmaxf(c[kb][2], c[kb][3]));
+    return fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3]));
+}
+
+template <typename TOut, int TPW, bool MULTI>
+__global__ __launch_bounds__(256, 1) void mha_hd64_direct16_kernel(FwdArgs a) {
+    static_assert(TPW >= 2 && TPW <= 4, "tiles per wave");
+    constexpr int KW = 4;                           // waves (key slices)
+    constexpr int BLOCK_M = 16;                     // query rows per workgroup
+    constexpr int WAVE_KEYS = kTileKV * TPW;
+    constexpr int OROW = 68;                        // epilogue fp32 row pitch
+    constexpr int EPI_WAVE = BLOCK_M * OROW * 4;
+    constexpr int RS = TPW * kTileBytes > EPI_WAVE ? TPW * kTileBytes : EPI_WAVE;
+    constexpr int LDS_BYTES = KW * RS + KW * BLOCK_M * 2 * 4;
+    static_assert(RS % 128 == 0 && LDS_BYTES <= 160 * 1024, "LDS layout");
+    __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+    lds_char* const lds = (lds_char*)smem;
+
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lane = tid & 63;
+    const int i16 = lane & 15;  // query column of the MFMA tiles
+    const int g = lane >> 4;    // operand k-group / result row group
+    // XCD-aware order (as the other kernels): consecutive j share an XCD and its L2
+    int qtile, bh, j;
+    {
+        const int T = a.total_blocks, L = blockIdx.x;
+        const int q8 = T >> 3, r8 = T & 7, xcd = L & 7;
+        j = xcd * q8 + min(xcd, r8) + (L >> 3);
+    }
+    int ci = 0;
+    if constexpr (MULTI) {
+#pragma unroll
+        for (int i = 1; i < kMaxCalls; ++i) ci += (int)((i < a.n_calls) & (j >= a.c[i].block_begin));
+    }
+    const CallArgs ca = MULTI ? pick_call(a, ci) : a.c[0];
+    {
+        const int jl = j - ca.block_begin;
+        qtile = jl % ca.qtiles;
+        bh = jl / ca.qtiles;
+    }
+    const int nq = ca.nq, nkv = ca.nkv;
+    const f16* Qb = reinterpret_cast<const f16*>(ca.q) + (size_t)bh * nq * kHeadDim;
+    const f16* Kb = reinterpret_cast<const f16*>(ca.k) + (size_t)bh * nkv * kHeadDim;
+    const f16* Vb = reinterpret_cast<const f16*>(ca.v) + (size_t)bh * nkv * kHeadDim;
+    const __amdgpu_buffer_rsrc_t q_rs = make_rsrc(Qb, (unsigned)nq * kHeadDim * 2);
+    const __amdgpu_buffer_rsrc_t k_rs = make_rsrc(Kb, (unsigned)nkv * kHeadDim * 2);
+    const __amdgpu_buffer_rsrc_t v_rs = make_rsrc(Vb, (unsigned)nkv * kHeadDim * 2);
+    const int q_row = qtile * BLOCK_M + i16;
+    const int key0 = wave * WAVE_KEYS;
+    const int n_t = max(0, min(TPW, (nkv - key0 + kTileKV - 1) / kTileKV));
+    const unsigned region = (unsigned)wave * RS;
+
+    f32x4 o[4];  // Oᵀ: dims 16db + 4g + j of query i16
+    f32x4 l_acc;
+    float m_run = 0.f;
+
+    if (n_t == 0) {  // a wave wholly past nkv contributes nothing (m = -inf in the merge)
+#pragma unroll
+        for (int db = 0; db < 4; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+        l_acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+        // ---- loads, all up front (rows past nkv / nq read as zero through the descriptors) ----
+        // DMA piece i = rows 8i..8i+7 of the wave's slice; lane L writes LDS chunk L&7 of row
+        // 8i + L/8 and reads the source chunk that the image puts there.
+        const unsigned lrow = (unsigned)(key0 + (lane >> 3)) * kHeadDim * 2;
+        const unsigned k_lane[2] = {lrow + (((lane & 7) ^ ((lane >> 4) & 7)) << 4),
+                                    lrow + (((lane & 7) ^ ((4 + (lane >> 4)) & 7)) << 4)};
+        const unsigned v_lane_off = lrow + (((lane & 7) ^ (((lane >> 4) & 3) << 1)) << 4);
+        auto dma_piece = [&](__amdgpu_buffer_rsrc_t rs, unsigned voff, int i) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * i),
+                                                     16, voff, 1024 * i, 0, 0);
+        };
+        auto dma_k = [&](int t0, int t1) {
+#pragma unroll
+            for (int i = 8 * t0; i < 8 * t1; ++i) dma_piece(k_rs, k_lane[i & 1], i);
+        };
+        auto dma_v = [&](int t) {
+#pragma unroll
+            for (int i = 8 * t; i < 8 * t + 8; ++i) dma_piece(v_rs, v_lane_off, i);
+        };
+        // K fragments of tile t (A operand of Sᵀ = K·Qᵀ): kf[kb][s] = K[64t+16kb+i16][32s+8g..+7]
+        auto read_k = [&](int t, f16x8(&kf)[4][2]) {
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    kf[kb][s] = lds_read16(lds, region + k_off(kTileKV * t + 16 * kb + i16, 4 * s + g));
+        };
+        // Q (B operand of Sᵀ = K·Qᵀ): Q[q_row][32s+8g..+7], by inline-asm loads (outside the
+        // compiler's wait bookkeeping, which would drain every DMA at their use)
+        f16x8 qraw[2], qf[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+            asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen"
+                         : "=v"(qraw[s])
+                         : "v"((unsigned)(q_row * kHeadDim + 32 * s + 8 * g) * 2), "s"(q_rs));
+        dma_k(0, 2);
+        wait_vmc<8>();  // Q and K(0) landed (younger: K(1))
+        asm volatile("" : "+v"(qraw[0]), "+v"(qraw[1])::"memory");
+        dma_k(2, TPW);
+        {
+            const float sc = kScaleLog2;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const u32x4 in = __builtin_bit_cast(u32x4, qraw[s]);
+                u32x4 outv;
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[1,0,0]\n\t"
+                        "v_fma_mixhi_f16 %0, %1, %2, 0 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                        : "=&v"(outv[w])
+                        : "v"(in[w]), "v"(sc));
+                qf[s] = __builtin_bit_cast(f16x8, outv);
+            }
+        }
+        const f16x8 ones = f16x8{1, 1, 1, 1, 1, 1, 1, 1};
+        // V tr-read bases: lane 4qq+pp of group g reads row 4g+qq (+ tile/step/half constants),
+        // dims 16db + 4pp..+3: chunk 2db + pp/2 at image position 2(db ^ sw) + pp/2
+        const int qq = (lane & 15) >> 2, pp = lane & 3;
+        const int sw = ((4 * g + qq) >> 1) & 3;
+        unsigned vbase[4];
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+            vbase[db] = region + (unsigned)(4 * g + qq) * 128 + ((2 * (db ^ sw) + (pp >> 1)) << 4) + 8 * (pp & 1);
+
+        f16x8 p[TPW][2];   // P (fp16), B operand of step u of tile t
+        f32x4 sc[TPW][4];  // raw scores of tiles 1..
+        auto pv = [&](int t) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const unsigned off = (unsigned)(t * kTileBytes + 128 * 32 * u);
+#pragma unroll
+                for (int db = 0; db < 4; ++db) {
+                    const f16x8 va = cat8(tr_read(lds, vbase[db] + off), tr_read(lds, vbase[db] + off + 16 * 128));
+                    const bool first = t == 0 && u == 0;
+                    o[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, p[t][u], first ? f32x4{} : o[db], 0, 0, 0);
+                }
+                l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, p[t][u], (t == 0 && u == 0) ? f32x4{} : l_acc, 0,
+                                                               0, 0);
+            }
+        };
+        auto exp_pack = [&](f32x4(&c)[4], f16x8(&pt)[2], float m) {
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) c[kb][e] = __builtin_amdgcn_exp2f(c[kb][e] - m);
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                pt[u] = f16x8{(f16)c[2 * u][0],     (f16)c[2 * u][1],     (f16)c[2 * u][2],     (f16)c[2 * u][3],
+                              (f16)c[2 * u + 1][0], (f16)c[2 * u + 1][1], (f16)c[2 * u + 1][2], (f16)c[2 * u + 1][3]};
+        };
+
+        // Phase 1, while V streams in: every tile's scores; the first tile's probabilities.
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+            f16x8 kf[4][2];
+            if (t > 0) wait_vmc<8 * (TPW - 1)>();  // K(t) landed: younger are K(t+1..), V(0..t-1)
+            read_k(t, kf);
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[1][0]), "+v"(kf[1][1]), "+v"(kf[2][0]),
+                           "+v"(kf[2][1]), "+v"(kf[3][0]), "+v"(kf[3][1])::"memory");
+            dma_v(t);  // over slot t, whose K is in registers
+            f32x4 c[4];
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb) {
+                c[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kb][0], qf[0], f32x4{}, 0, 0, 0);
+                c[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kb][1], qf[1], c[kb], 0, 0, 0);
+            }
+            if (key0 + kTileKV * (t + 1) > nkv) {  // wave-uniform: mask keys past nkv
+#pragma unroll
+                for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (key0 + kTileKV * t + 16 * kb + 4 * g + e >= nkv) c[kb][e] = -INFINITY;
+            }
+            if (t == 0) {
+                const float mx = xquad_max(max16(c));
+                m_run = (mx < kEmptyMax) ? 0.f : mx;  // a fully masked tile: m = 0
+                exp_pack(c, p[0], m_run);
+            } else {
+#pragma unroll
+                for (int kb = 0; kb < 4; ++kb) sc[t][kb] = c[kb];
+            }
+        }
+        // ONE rescale decision for the later tiles (wave-uniform, rare): move the max by the
+        // largest excess over kRescaleThr, rescaling the first tile's probabilities.
+        {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int t = 1; t < TPW; ++t) mx = fmaxf(mx, max16(sc[t]));
+            const float ex = xquad_max(mx) - m_run;
+            if (__builtin_amdgcn_ballot_w64(ex > kRescaleThr) != 0) {
+                const float d = fmaxf(ex, 0.f);
+                const f16 alpha = (f16)__builtin_amdgcn_exp2f(-d);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) p[0][u] *= alpha;
+                m_run += d;
+            }
+        }
+        wait_vmc<8 * (TPW - 1)>();  // V(0) landed
+        pv(0);                      // beside the later tiles' exponentials
+#pragma unroll
+        for (int t = 1; t < TPW; ++t) exp_pack(sc[t], p[t], m_run);
+        wait_vmc<0>();
+#pragma unroll
+        for (int t = 1; t < TPW; ++t) pv(t);
+    }
+
+    // ---- epilogue: merge the 4 key slices through LDS ----
+    float* ol = reinterpret_cast<float*>(smem + region);     // [16][OROW]
+    float* mlb = reinterpret_cast<float*>(smem + KW * RS);  // [KW][16][2]
+    {
+        const float L_w = l_acc[0];
+        const float m_w = (L_w > 0.f) ? m_run : -INFINITY;
+        float* dst = ol + i16 * OROW + 4 * g;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) *reinterpret_cast<f32x4*>(dst + 16 * db) = o[db];
+        if (g == 0) *reinterpret_cast<float2*>(mlb + (wave * BLOCK_M + i16) * 2) = make_float2(m_w, L_w);
+    }
+    __syncthreads();
+    const int row = tid >> 4, c = (tid & 15) * 4;
+    const int q = qtile * BLOCK_M + row;
+    float2 ml[KW];
+    float M = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+        ml[k] = *reinterpret_cast<const float2*>(mlb + (k * BLOCK_M + row) * 2);
+        M = fmaxf(M, ml[k].x);
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    float L = 0.f;
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+        const float w = (ml[k].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[k].x - M);
+        L += w * ml[k].y;
+        acc += w * *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(smem + k * RS) + row * OROW + c);
+    }
+    if (q < nq) {
+        const __amdgpu_buffer_rsrc_t o_rs = make_rsrc(reinterpret_cast<TOut*>(ca.o) + (size_t)bh * nq * kHeadDim,
+                                                      (unsigned)(nq * kHeadDim * sizeof(TOut)));
+        const float inv = 1.f / L;
+        store_dims<TOut, 4, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)), acc * inv, acc * inv);
+    }
+}
+
+template <typename TOut, int TPW>
+hipError_t launch16_t(const FwdArgs& a, int grid, hipStream_t stream) {
+    if (a.n_calls > 1)
+        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, TPW, true>), dim3(grid), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, TPW, false>), dim3(grid), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_direct16(const FwdArgs& a, int grid, int tiles_per_wave, bool out_f32, hipStream_t stream) {
+    // tiles_per_wave counts 64-key tiles per wave of the 8-wave form (1: nkv <= 512, 2: <= 1024);
+    // 4 waves take twice as many
+    switch (tiles_per_wave * 2 + (out_f32 ? 1 : 0)) {
+        case 2: return launch16_t<f16, 2>(a, grid, stream);
+        case 3: return launch16_t<float, 2>(a, grid, stream);
+        case 4: return launch16_t<f16, 4>(a, grid, stream);
+        case 5: return launch16_t<float, 4>(a, grid, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace mha_hd64

@@ -32,7 +32,7 @@ struct Call {
 struct LaunchPlan {
     int q_waves;          // waves per workgroup that own distinct 32-row query slices
     int kv_waves;         // waves per workgroup that split the keys of every iteration
-    int rows_per_wave;    // 32, or 64 (two query blocks per wave)
+    int rows_per_wave;    // 32, or 64 (two query blocks per wave); 16: the 16-row single-pass kernel
     int splits;           // KV split across workgroups (1 = no combine pass)
     int tiles_per_split;  // KV super-tiles (64 * kv_waves keys) per split
     size_t ws_needed;     // workspace bytes the plan uses
@@ -56,6 +56,8 @@ struct GroupPlan {
 };
 // force_q_waves = kForceDirect selects the single-pass kernel (fp16 input, nkv <= 1024).
 constexpr int kForceDirect = 21;
+// force_q_waves = kForceDirect16 selects the 16-row single-pass kernel (mha_hd64_direct16.hip).
+constexpr int kForceDirect16 = 22;
 GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_waves = 0, int force_kv_waves = 0,
                      int force_splits = 0, InType in = InType::F16);
 hipError_t launch_group(const Call* calls, int n, InType in, OutType out, void* workspace, size_t ws_bytes,

@@ -980,21 +980,46 @@ static bool direct_enabled() {
 // Tiles of 64 keys per wave of the single-pass kernel for this launch, or 0 if it does not apply:
 // fp16 input, every call's keys within 8 waves x 2 tiles, and at most 256 workgroups of 32 rows
 // (one residency round: the launches the ring kernel can only fill by splitting the keys).
-static int direct_tiles_for(const Call* calls, int n, InType in, bool forced) {
+static int direct_tiles_for(const Call* calls, int n, InType in, bool forced, int rows = 32) {
     if (in != InType::F16 || (!forced && !direct_enabled())) return 0;
     long wgs = 0;
     int tiles = 1;
     for (int i = 0; i < n; ++i) {
         if (calls[i].nkv > 8 * 2 * kTileKV) return 0;
         tiles = std::max(tiles, (calls[i].nkv + 8 * kTileKV - 1) / (8 * kTileKV));
-        wgs += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 31) / 32);
+        wgs += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + rows - 1) / rows);
     }
     return (forced || wgs <= 256) ? tiles : 0;
+}
+
+// The 16-row single-pass kernel first (default; MHA_HD64_DIRECT_ROWS=32 keeps 32-row blocks)
+static bool direct16_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("MHA_HD64_DIRECT_ROWS");
+        return !(e && e[0] == '3');
+    }();
+    return on;
 }
 
 GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_waves, int force_kv_waves,
                      int force_splits, InType in) {
     GroupPlan p{};
+    // 16-row blocks first: a launch of at most 256 of them runs every block on its own CU
+    if (force_q_waves == kForceDirect16 || (force_q_waves == 0 && direct16_enabled())) {
+        const int dt = direct_tiles_for(calls, n, in, force_q_waves == kForceDirect16, 16);
+        if (dt > 0) {
+            p.q_waves = 1;
+            p.kv_waves = 4;
+            p.rows_per_wave = 16;
+            p.direct_tiles = dt;
+            for (int i = 0; i < n; ++i) {
+                p.splits[i] = 1;
+                p.tiles_per_split[i] = 1;
+            }
+            return p;
+        }
+        if (force_q_waves == kForceDirect16) force_q_waves = 0;  // not applicable: the planner's choice
+    }
     if (force_q_waves == kForceDirect || force_q_waves == 0) {
         const int dt = direct_tiles_for(calls, n, in, force_q_waves == kForceDirect);
         if (dt > 0) {
@@ -1128,7 +1153,8 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
         ca.splits = p.splits[i];
         ca.tiles_per_split = p.tiles_per_split[i];
         ca.bh = c.batch * c.heads;
-        ca.qtiles = (c.nq + 32 * p.q_waves * (p.rows_per_wave / 32) - 1) / (32 * p.q_waves * (p.rows_per_wave / 32));
+        const int block_m = p.rows_per_wave == 16 ? 16 : 32 * p.q_waves * (p.rows_per_wave / 32);
+        ca.qtiles = (c.nq + block_m - 1) / block_m;
         ca.block_begin = blocks;
         if (ca.splits > 1) {
             const size_t rows = (size_t)ca.bh * ca.splits * c.nq;
@@ -1154,7 +1180,8 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
     if (p.direct_tiles > 0) {  // single-pass kernel: no split, no workspace
         g_last_combine = 0;
         if (!(phase_mask & 1)) return hipSuccess;
-        return launch_direct(a, blocks, p.direct_tiles, out == OutType::F32, stream);
+        return p.rows_per_wave == 16 ? launch_direct16(a, blocks, p.direct_tiles, out == OutType::F32, stream)
+                                     : launch_direct(a, blocks, p.direct_tiles, out == OutType::F32, stream);
     }
     // Split calls combine inside the main launch when a ticket array is available (phase_mask 3,
     // the production form); otherwise (or MHA_HD64_FUSED_COMBINE=0) in the combine kernel.

@@ -211,15 +211,15 @@ def test_launch_rejects_misaligned_and_null(lib):
 def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
     out = (ctypes.c_int32 * 4)()
     # metric shape 1x4x1024x1024 inside the fixed 5,242,880 B workspace
-    # (single-pass kernel, plan code 21: 128 workgroups of 32 rows x all 1024 keys, no split,
-    # no workspace)
+    # (16-row single-pass kernel, plan code 22: 256 workgroups of 16 rows x all 1024 keys, no
+    # split, no workspace)
     need = lib.mha_hd64_plan(1, 4, 1024, 1024, 5242880, out)
     qw, kw, splits, tps = list(out)
-    assert need == 0 and (qw, kw, splits) == (21, 8, 1)
+    assert need == 0 and (qw, kw, splits) == (22, 4, 1)
     # past 1024 keys the ring kernel splits the keys within the fixed workspace
     need = lib.mha_hd64_plan(1, 4, 1024, 2048, 5242880, out)
     qw, kw, splits, tps = list(out)
-    assert need <= 5242880 and splits >= 2 and qw != 21
+    assert need <= 5242880 and splits >= 2 and qw not in (21, 22)
     # max length still fits
     need = lib.mha_hd64_plan(1, 4, 2048, 2048, 5242880, out)
     assert need <= 5242880
@@ -231,24 +231,27 @@ def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
     assert out[2] == 1 and out[0] == 4
 
 
-@pytest.mark.parametrize("batch,nq,nkv,direct", [
-    (1, 1024, 1024, True),     # the metric call: 128 blocks of 32 rows, 1024 keys
-    (1, 2048, 1024, True),     # 256 blocks: still one residency round
-    (2, 2048, 1024, False),    # 512 blocks: the ring kernel fills the chip by itself
-    (1, 1024, 1025, False),    # more keys than 8 waves x 2 tiles
-    (1, 256, 256, True),
-    (1, 1, 1, True),
-    (8, 1024, 1024, False),    # batched: 1024 blocks
-    (2, 1024, 512, True),
+@pytest.mark.parametrize("batch,nq,nkv,code", [
+    (1, 1024, 1024, 22),     # the metric call: 256 blocks of 16 rows, 1024 keys
+    (1, 2048, 1024, 21),     # 512 16-row blocks, 256 of 32 rows: the 32-row kernel
+    (2, 2048, 1024, None),   # 512 32-row blocks: the ring kernel fills the chip by itself
+    (1, 1024, 1025, None),   # more keys than 8 waves x 2 tiles
+    (1, 256, 256, 22),
+    (1, 1, 1, 22),
+    (8, 1024, 1024, None),   # batched: 1024 blocks
+    (2, 1024, 512, 21),
+    (2, 512, 1000, 22),
 ])
-def test_planner_single_pass_rule(lib, batch, nq, nkv, direct):
-    """plan code 21 (single-pass kernel) iff fp16, nkv <= 1024 and <= 256 32-row blocks; it needs
-    no workspace and never splits."""
+def test_planner_single_pass_rule(lib, batch, nq, nkv, code):
+    """Single-pass kernels iff fp16 and nkv <= 1024: plan code 22 (16-row blocks) when at most 256
+    of them, else 21 (32-row blocks) when at most 256 of those; they need no workspace and never
+    split."""
     out = (ctypes.c_int32 * 4)()
     need = lib.mha_hd64_plan(batch, 4, nq, nkv, 5242880, out)
-    assert (out[0] == 21) == direct
-    if direct:
-        assert need == 0 and out[2] == 1
+    if code is None:
+        assert out[0] not in (21, 22)
+    else:
+        assert out[0] == code and need == 0 and out[2] == 1
 
 
 def test_abort_mode_aborts_like_plugin_assert():

@@ -465,15 +465,18 @@ def test_fused_combine_graphs_from_one_stream_replayed_concurrently(dev):
             assert torch.equal(d[4], d[3])
 
 
-# ---- single-pass kernel (csrc/mha_hd64_direct.hip; forced plan 21, the planner's choice for
-# fp16 launches of <= 256 32-row blocks with nkv <= 1024) ----
+# ---- single-pass kernels (csrc/mha_hd64_direct16.hip, forced plan 22: the planner's choice for
+# fp16 launches of <= 256 16-row blocks with nkv <= 1024; csrc/mha_hd64_direct.hip, plan 21: <= 256
+# 32-row blocks) ----
 DIRECT_SHAPES = [(1, 1), (33, 65), (100, 77), (256, 256), (1000, 777), (1024, 1024), (64, 1024), (513, 513),
                  (2048, 1000), (300, 129), (97, 600), (5, 1024), (1024, 64), (130, 520)]
 
 
+@pytest.mark.parametrize("code", [21, 22])
 @pytest.mark.parametrize("nq,nkv", DIRECT_SHAPES)
-def test_direct_kernel_matches_oracle(nq, nkv, dev, oracle_mod):
-    """Every key-tile layout: waves wholly past nkv, partial tiles, one- and two-tile waves."""
+def test_direct_kernel_matches_oracle(nq, nkv, code, dev, oracle_mod):
+    """Every key-tile layout: waves wholly past nkv, partial tiles, one- and two-tile waves; the
+    32-row (code 21) and 16-row (code 22) single-pass kernels."""
     from lightglue_amd import _lib, synth
 
     lib = _lib.load()
@@ -485,7 +488,7 @@ def test_direct_kernel_matches_oracle(nq, nkv, dev, oracle_mod):
     ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
     for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
         o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
-        _forced(lib, q, k, v, o, nq, nkv, 21, 0, 0, ws)
+        _forced(lib, q, k, v, o, nq, nkv, code, 0, 0, ws)
         assert lib.mha_hd64_last_combine_form() == 0
         torch.cuda.synchronize()
         got = o.float().cpu().numpy()
@@ -507,10 +510,11 @@ def test_direct_kernel_rescale_and_masked_waves(dev, oracle_mod):
         q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
         ref = oracle_mod.attention_c(q16, k16, v16)
         q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
-        o = torch.empty_like(q)
-        _forced(lib, q, k, v, o, nq, nkv, 21, 0, 0, ws)
-        torch.cuda.synchronize()
-        assert _maxdiff(o.float().cpu().numpy(), ref) <= TOL, (nkv, krow, gain)
+        for code in (21, 22):
+            o = torch.empty_like(q)
+            _forced(lib, q, k, v, o, nq, nkv, code, 0, 0, ws)
+            torch.cuda.synchronize()
+            assert _maxdiff(o.float().cpu().numpy(), ref) <= TOL, (code, nkv, krow, gain)
 
 
 def test_direct_kernel_grouped_and_batched(dev, oracle_mod):
@@ -546,10 +550,11 @@ def test_direct_kernel_forced_outside_its_range_is_rejected(dev):
         q = torch.zeros(1, 4, 64, 64, dtype=dt, device=dev)
         k = torch.zeros(1, 4, nkv, 64, dtype=dt, device=dev)
         o = torch.empty_like(q)
-        st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), k.data_ptr(), o.data_ptr(), 1, 4, 64, nkv,
-                                        int(dt == torch.float32), int(dt == torch.float32), 21, 0, 0,
-                                        ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream, 3)
-        assert st == 1, (nkv, dt)
+        for code in (21, 22):
+            st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), k.data_ptr(), o.data_ptr(), 1, 4, 64, nkv,
+                                            int(dt == torch.float32), int(dt == torch.float32), code, 0, 0,
+                                            ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream, 3)
+            assert st == 1, (code, nkv, dt)
 
 
 def test_direct_kernel_deterministic_and_capturable(dev):

@@ -9,7 +9,7 @@ mkdir -p lib/exp
 make -s lib/libmha_hd64.so
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans "$@" \
       -I../include -Icsrc -c csrc/mha_hd64_direct.hip -o lib/exp/d_$NAME.o
-hipcc --offload-arch=gfx950 -shared -fPIC lib/obj/mha_hd64_kernels.o lib/exp/d_$NAME.o lib/obj/mha_hd64_plugin.o \
+hipcc --offload-arch=gfx950 -shared -fPIC lib/obj/mha_hd64_kernels.o lib/exp/d_$NAME.o lib/obj/mha_hd64_direct16.o lib/obj/mha_hd64_plugin.o \
       lib/obj/lightglue_glue.o lib/obj/lightglue_linear.o -o lib/exp/libmha_hd64_$NAME.so
 rm -f lib/exp/d_$NAME.o
 echo lib/exp/libmha_hd64_$NAME.so

@@ -63,20 +63,23 @@ def main():
             q, k, v = (torch.from_numpy(x).to(dev).half().contiguous() for x in (q16, k16, v16))
             for of in (0, 1):
                 o = torch.full(q.shape, float("nan"), dtype=torch.float32 if of else torch.float16, device=dev)
-                forced(lib, q, k, v, o, nq, nkv, 21, 0, 0, ws)
-                torch.cuda.synchronize()
-                got = o.float().cpu().numpy()
-                errs[f"{nq}x{nkv}_{'f32' if of else 'f16'}"] = (float(np.abs(got - ref).max())
-                                                               if np.isfinite(got).all() else "nonfinite")
+                for code in (21, 22):
+                    o.fill_(float("nan"))
+                    forced(lib, q, k, v, o, nq, nkv, code, 0, 0, ws)
+                    torch.cuda.synchronize()
+                    got = o.float().cpu().numpy()
+                    errs[f"{code}_{nq}x{nkv}_{'f32' if of else 'f16'}"] = (float(np.abs(got - ref).max())
+                                                                          if np.isfinite(got).all() else "nonfinite")
         # peaky logits (rescale branch)
         qn, kn, vn = synth.qkv(4242, 256, 1024, q_std=3.0)
         q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
         ref = oracle.attention_c(q16, k16, v16)
         q, k, v = (torch.from_numpy(x).to(dev).half().contiguous() for x in (q16, k16, v16))
         o = torch.empty_like(q)
-        forced(lib, q, k, v, o, 256, 1024, 21, 0, 0, ws)
-        torch.cuda.synchronize()
-        errs["peaky256x1024"] = float(np.abs(o.float().cpu().numpy() - ref).max())
+        for code in (21, 22):
+            forced(lib, q, k, v, o, 256, 1024, code, 0, 0, ws)
+            torch.cuda.synchronize()
+            errs[f"{code}_peaky256x1024"] = float(np.abs(o.float().cpu().numpy() - ref).max())
         res["max_abs_err"] = errs
     for n in (512, 1024):
         qn, kn, vn = synth.qkv(5, n, n)
@@ -85,7 +88,9 @@ def main():
         t_direct = per_launch_us(lambda: forced(lib, q, k, v, o, n, n, 21, 0, 0, ws))
         t_ring = per_launch_us(lambda: forced(lib, q, k, v, o, n, n, 1, 8, 0, ws))
         t_direct2 = per_launch_us(lambda: forced(lib, q, k, v, o, n, n, 21, 0, 0, ws))
-        res[f"us_{n}"] = {"direct": round(min(t_direct, t_direct2), 3), "ring_1x8": round(t_ring, 3)}
+        t16 = per_launch_us(lambda: forced(lib, q, k, v, o, n, n, 22, 0, 0, ws))
+        res[f"us_{n}"] = {"direct": round(min(t_direct, t_direct2), 3), "direct16": round(t16, 3),
+                          "ring_1x8": round(t_ring, 3)}
     print(json.dumps(res))
 
 

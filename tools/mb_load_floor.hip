@@ -53,8 +53,8 @@ __global__ __launch_bounds__(NT) void stream_kernel(const u32x4* K, const u32x4*
 
 // The same volume by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per instruction) into a 16 KiB
 // per-wave LDS region (overwritten in turn: only the transfer rate is of interest).
-template <int KPW>
-__global__ __launch_bounds__(512) void dma_kernel(const u32x4* K, const u32x4* V, u32x4* O, int span) {
+template <int KPW, int NT = 512>
+__global__ __launch_bounds__(NT) void dma_kernel(const u32x4* K, const u32x4* V, u32x4* O, int span) {
     __shared__ __attribute__((aligned(16))) char lds[8 * 16384];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int xcd = blockIdx.x & 7, idx = blockIdx.x >> 3;
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(512) void dma_kernel(const u32x4* K, const u32x4* V
                                                  (unsigned)(key0 * 128 + lane * 16), i * 1024, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    O[(size_t)blockIdx.x * 512 + threadIdx.x] = *(const u32x4*)(lds + threadIdx.x * 16);
+    O[(size_t)blockIdx.x * NT + threadIdx.x] = *(const u32x4*)(lds + threadIdx.x * 16);
 }
 
 __global__ void empty_kernel() {}
@@ -135,6 +135,11 @@ int main() {
            time_graph([&] { dma_kernel<128><<<128, 512, 0, s>>>(K, V, O, 1024); }, s, C));
     printf(", \"dma_split2_256x512_kpw64_us\": %.3f",
            time_graph([&] { dma_kernel<64><<<256, 512, 0, s>>>(K, V, O, 512); }, s, C));
+    RUN("nosplit16_256x256_kpw256_us", 256, 256, 256, 1024); // 16 rows x 1024 keys, 4 waves
+    printf(", \"dma_nosplit_128x256_kpw256_us\": %.3f",
+           time_graph([&] { dma_kernel<256, 256><<<128, 256, 0, s>>>(K, V, O, 1024); }, s, C));
+    printf(", \"dma_nosplit16_256x256_kpw256_us\": %.3f",
+           time_graph([&] { dma_kernel<256, 256><<<256, 256, 0, s>>>(K, V, O, 1024); }, s, C));
     printf("}\n");
     return 0;
 }
