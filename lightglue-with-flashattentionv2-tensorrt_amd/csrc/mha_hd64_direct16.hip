@@ -31,6 +31,27 @@
 #include "mha_hd64_device.h"
 #include "mha_hd64_internal.h"
 
+// Diagnostic timestamps (-DMHA_STAMPS builds, tools/dstamps.py ... 22): wave 0's s_memtime at the
+// phase boundaries of mha_hd64_direct.hip's slots (0 entry, 1 Q + K(0) landed, 3 V(0) landed,
+// 2 later tiles' exponentials done, 4 PV done, 5 after the epilogue barrier, 6 stores acked).
+#ifdef MHA_STAMPS
+#define DSTAMP(slot)                                                                              \
+    do {                                                                                          \
+        unsigned long long t_;                                                                    \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                \
+        if (threadIdx.x == 0) a.stamps[blockIdx.x * 8 + (slot)] = t_;                             \
+    } while (0)
+#else
+#define DSTAMP(slot) \
+    do {             \
+    } while (0)
+#endif
+
+#ifndef MHA_D16_WAVES
+#define MHA_D16_WAVES 4  // waves per workgroup for nkv in (512, 1024]; 8 (8 x 2 tiles, two waves per
+                         // SIMD) measured 5.23 against 4.89 us at 1x4x1024^2: an A/B hook only
+#endif
+
 namespace mha_hd64 {
 namespace {
 
@@ -58,10 +79,9 @@ __device__ __forceinline__ float max16(const f32x4 (&c)[4]) {
     return fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3]));
 }
 
-template <typename TOut, int TPW, bool MULTI>
-__global__ __launch_bounds__(256, 1) void mha_hd64_direct16_kernel(FwdArgs a) {
-    static_assert(TPW >= 2 && TPW <= 4, "tiles per wave");
-    constexpr int KW = 4;                           // waves (key slices)
+template <typename TOut, int KW, int TPW, bool MULTI>
+__global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(FwdArgs a) {
+    static_assert(TPW >= 2 && TPW <= 4 && (KW == 4 || KW == 8), "waves x tiles per wave");
     constexpr int BLOCK_M = 16;                     // query rows per workgroup
     constexpr int WAVE_KEYS = kTileKV * TPW;
     constexpr int OROW = 68;                        // epilogue fp32 row pitch
@@ -72,6 +92,7 @@ __global__ __launch_bounds__(256, 1) void mha_hd64_direct16_kernel(FwdArgs a) {
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     lds_char* const lds = (lds_char*)smem;
 
+    DSTAMP(0);
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
@@ -154,6 +175,7 @@ __global__ __launch_bounds__(256, 1) void mha_hd64_direct16_kernel(FwdArgs a) {
         dma_k(0, 2);
         wait_vmc<8>();  // Q and K(0) landed (younger: K(1))
         asm volatile("" : "+v"(qraw[0]), "+v"(qraw[1])::"memory");
+        DSTAMP(1);
         dma_k(2, TPW);
         {
             const float sc = kScaleLog2;
@@ -255,13 +277,16 @@ __global__ __launch_bounds__(256, 1) void mha_hd64_direct16_kernel(FwdArgs a) {
             }
         }
         wait_vmc<8 * (TPW - 1)>();  // V(0) landed
+        DSTAMP(3);
         pv(0);                      // beside the later tiles' exponentials
 #pragma unroll
         for (int t = 1; t < TPW; ++t) exp_pack(sc[t], p[t], m_run);
+        DSTAMP(2);
         wait_vmc<0>();
 #pragma unroll
         for (int t = 1; t < TPW; ++t) pv(t);
     }
+    DSTAMP(4);
 
     // ---- epilogue: merge the 4 key slices through LDS ----
     float* ol = reinterpret_cast<float*>(smem + region);     // [16][OROW]
@@ -275,6 +300,8 @@ __global__ __launch_bounds__(256, 1) void mha_hd64_direct16_kernel(FwdArgs a) {
         if (g == 0) *reinterpret_cast<float2*>(mlb + (wave * BLOCK_M + i16) * 2) = make_float2(m_w, L_w);
     }
     __syncthreads();
+    DSTAMP(5);
+    if (KW > 4 && tid >= 256) return;  // 256 threads merge (row, 4 dims)
     const int row = tid >> 4, c = (tid & 15) * 4;
     const int q = qtile * BLOCK_M + row;
     float2 ml[KW];
@@ -298,14 +325,18 @@ __global__ __launch_bounds__(256, 1) void mha_hd64_direct16_kernel(FwdArgs a) {
         const float inv = 1.f / L;
         store_dims<TOut, 4, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)), acc * inv, acc * inv);
     }
+#ifdef MHA_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    DSTAMP(6);
+#endif
 }
 
-template <typename TOut, int TPW>
+template <typename TOut, int KW, int TPW>
 hipError_t launch16_t(const FwdArgs& a, int grid, hipStream_t stream) {
     if (a.n_calls > 1)
-        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, TPW, true>), dim3(grid), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, true>), dim3(grid), dim3(64 * KW), 0, stream, a);
     else
-        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, TPW, false>), dim3(grid), dim3(256), 0, stream, a);
+        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, false>), dim3(grid), dim3(64 * KW), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -315,10 +346,15 @@ hipError_t launch_direct16(const FwdArgs& a, int grid, int tiles_per_wave, bool 
     // tiles_per_wave counts 64-key tiles per wave of the 8-wave form (1: nkv <= 512, 2: <= 1024);
     // 4 waves take twice as many
     switch (tiles_per_wave * 2 + (out_f32 ? 1 : 0)) {
-        case 2: return launch16_t<f16, 2>(a, grid, stream);
-        case 3: return launch16_t<float, 2>(a, grid, stream);
-        case 4: return launch16_t<f16, 4>(a, grid, stream);
-        case 5: return launch16_t<float, 4>(a, grid, stream);
+        case 2: return launch16_t<f16, 4, 2>(a, grid, stream);
+        case 3: return launch16_t<float, 4, 2>(a, grid, stream);
+#if MHA_D16_WAVES == 8
+        case 4: return launch16_t<f16, 8, 2>(a, grid, stream);
+        case 5: return launch16_t<float, 8, 2>(a, grid, stream);
+#else
+        case 4: return launch16_t<f16, 4, 4>(a, grid, stream);
+        case 5: return launch16_t<float, 4, 4>(a, grid, stream);
+#endif
         default: return hipErrorInvalidValue;
     }
 }

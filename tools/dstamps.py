@@ -1,6 +1,6 @@
 """Diagnostic: phase timestamps of the single-pass kernel from a -DMHA_STAMPS build
 (tools/build_direct_variant.sh stamps -DMHA_STAMPS).
-    python tools/dstamps.py <lib.so> nq nkv
+    python tools/dstamps.py <lib.so> nq nkv [plan code: 21 (32-row kernel, default) | 22 (16-row)]
 Slots (wave 0 of every workgroup, s_memtime cycles): 0 entry, 1 Q + K(0) landed, 2 scores and
 probabilities of every tile done, 3 V(0) landed, 4 PV done, 5 after the epilogue barrier,
 6 output stores acknowledged. Prints medians / maxima of each segment and of the start spread."""
@@ -18,6 +18,8 @@ from lightglue_amd import _lib, synth  # noqa: E402
 _lib.LIB_PATH = os.path.abspath(sys.argv[1])
 lib = _lib.load()
 nq, nkv = int(sys.argv[2]), int(sys.argv[3])
+code = int(sys.argv[4]) if len(sys.argv) > 4 else 21
+rows = 16 if code == 22 else 32
 dev = torch.device("cuda:0")
 qn, kn, vn = synth.qkv(3, nq, nkv)
 q, k, v = (torch.from_numpy(x).to(dev).half().contiguous() for x in (qn, kn, vn))
@@ -28,10 +30,10 @@ lib.mha_hd64_set_stamp_buffer(st.data_ptr())
 s = torch.cuda.current_stream().cuda_stream
 res = []
 for rep in range(30):  # back-to-back launches (clocks up); keep the last
-    lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), 1, 4, nq, nkv, 0, 0, 21, 0, 0,
+    lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), 1, 4, nq, nkv, 0, 0, code, 0, 0,
                                ws.data_ptr(), ws.numel(), s, 3)
 torch.cuda.synchronize()
-nwg = -(-nq // 32) * 4
+nwg = -(-nq // rows) * 4
 t = st[: nwg * 8].view(nwg, 8).cpu().numpy().astype("int64")
 t0 = t[:, 0].min()
 d = {"nq": nq, "nkv": nkv, "wgs": nwg, "start_spread_cyc": int(t[:, 0].max() - t0),
