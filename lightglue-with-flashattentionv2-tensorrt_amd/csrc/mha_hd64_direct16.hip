@@ -80,7 +80,12 @@ __device__ __forceinline__ float max16(const f32x4 (&c)[4]) {
 }
 
 template <typename TOut, int KW, int TPW, bool MULTI>
-__global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(FwdArgs a) {
+// The single call's own arguments come first as plain scalars (q0 .. qtiles0: 12 dwords), so the
+// command processor can preload them into SGPRs (-amdgpu-kernarg-preload-count, Makefile) and the
+// first loads need no dependent kernarg fetch; grouped launches (MULTI) read the table `a`.
+__global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const void* q0, const void* k0, const void* v0,
+                                                                        void* o0, int total_blocks, int nq0, int nkv0,
+                                                                        int qtiles0, FwdArgs a) {
     static_assert(TPW >= 2 && TPW <= 4 && (KW == 4 || KW == 8), "waves x tiles per wave");
     constexpr int BLOCK_M = 16;                     // query rows per workgroup
     constexpr int WAVE_KEYS = kTileKV * TPW;
@@ -101,7 +106,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(FwdArgs a
     // XCD-aware order (as the other kernels): consecutive j share an XCD and its L2
     int qtile, bh, j;
     {
-        const int T = a.total_blocks, L = blockIdx.x;
+        const int T = total_blocks, L = blockIdx.x;
         const int q8 = T >> 3, r8 = T & 7, xcd = L & 7;
         j = xcd * q8 + min(xcd, r8) + (L >> 3);
     }
@@ -110,7 +115,19 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(FwdArgs a
 #pragma unroll
         for (int i = 1; i < kMaxCalls; ++i) ci += (int)((i < a.n_calls) & (j >= a.c[i].block_begin));
     }
-    const CallArgs ca = MULTI ? pick_call(a, ci) : a.c[0];
+    CallArgs ca;
+    if constexpr (MULTI) {
+        ca = pick_call(a, ci);
+    } else {
+        ca.q = q0;
+        ca.k = k0;
+        ca.v = v0;
+        ca.o = o0;
+        ca.nq = nq0;
+        ca.nkv = nkv0;
+        ca.qtiles = qtiles0;
+        ca.block_begin = 0;
+    }
     {
         const int jl = j - ca.block_begin;
         qtile = jl % ca.qtiles;
@@ -334,9 +351,12 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(FwdArgs a
 template <typename TOut, int KW, int TPW>
 hipError_t launch16_t(const FwdArgs& a, int grid, hipStream_t stream) {
     if (a.n_calls > 1)
-        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, true>), dim3(grid), dim3(64 * KW), 0, stream, a);
+        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, true>), dim3(grid), dim3(64 * KW), 0, stream,
+                           nullptr, nullptr, nullptr, nullptr, a.total_blocks, 0, 0, 0, a);
     else
-        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, false>), dim3(grid), dim3(64 * KW), 0, stream, a);
+        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, false>), dim3(grid), dim3(64 * KW), 0, stream,
+                           a.c[0].q, a.c[0].k, a.c[0].v, a.c[0].o, a.total_blocks, a.c[0].nq, a.c[0].nkv,
+                           a.c[0].qtiles, a);
     return hipGetLastError();
 }
 
