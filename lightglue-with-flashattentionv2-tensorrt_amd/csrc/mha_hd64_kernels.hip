@@ -1130,9 +1130,91 @@ LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves, int forc
     return p;
 }
 
+// ---- Float boundary onto the single-pass kernels ----
+// fp32 Q/K/V of launches the single-pass kernels take (as fp16) are rounded to fp16 (RNE, the
+// reference's convert kernel …fp16in_fp32out.cu:706-804 without its padding) into the caller's
+// workspace by one elementwise launch, then run there; the LDS-ring kernel converts on load instead.
+namespace {
+constexpr int kConvMax = 3 * kMaxCalls;
+struct ConvArgs {
+    const float* src[kConvMax];
+    f16* dst[kConvMax];
+    unsigned end8[kConvMax];  // prefix sums of each tensor's element count / 8
+    int count;
+};
+
+__global__ __launch_bounds__(256) void convert_f32_f16_kernel(ConvArgs c) {
+    const unsigned g = blockIdx.x * 256u + threadIdx.x;
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < kConvMax - 1; ++i) t += (int)((i < c.count - 1) & (g >= c.end8[i]));
+    if (g >= c.end8[t]) return;
+    const unsigned idx = g - (t ? c.end8[t - 1] : 0u);
+    const f32x4* s = reinterpret_cast<const f32x4*>(c.src[t]) + 2 * (size_t)idx;
+    const f32x4 lo = s[0], hi = s[1];
+    const f16x4 a = __builtin_convertvector(lo, f16x4), b = __builtin_convertvector(hi, f16x4);
+    reinterpret_cast<f16x8*>(c.dst[t])[idx] = f16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+bool f32_convert_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("MHA_HD64_F32_CONVERT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+}  // namespace
+
+static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutType out, void* workspace,
+                                     size_t ws_bytes, hipStream_t stream, int force_q_waves, int force_kv_waves,
+                                     int force_splits, int phase_mask);
+
+// The convert + single-pass form of an fp32-input launch, or hipErrorNotSupported when it does
+// not apply (not the planner's choice, no single-pass plan for these shapes, workspace too small).
+static hipError_t launch_f32_via_f16(const Call* calls, int n, OutType out, void* workspace, size_t ws_bytes,
+                                     hipStream_t stream, int phase_mask) {
+    if (!f32_convert_enabled() || !workspace) return hipErrorNotSupported;
+    if (plan_group(calls, n, 0, 0, 0, 0, InType::F16).direct_tiles == 0) return hipErrorNotSupported;
+    Call c16[kMaxCalls];
+    ConvArgs cv{};
+    size_t off = 0;
+    unsigned total8 = 0;
+    char* ws = reinterpret_cast<char*>(workspace);
+    for (int i = 0; i < n; ++i) {
+        c16[i] = calls[i];
+        if (calls[i].nq <= 0 || calls[i].batch <= 0 || calls[i].heads <= 0) continue;
+        const size_t bh = (size_t)calls[i].batch * calls[i].heads;
+        const size_t elems[3] = {bh * calls[i].nq * kHeadDim, bh * calls[i].nkv * kHeadDim,
+                                 bh * calls[i].nkv * kHeadDim};
+        const void* src[3] = {calls[i].q, calls[i].k, calls[i].v};
+        const void** dstp[3] = {&c16[i].q, &c16[i].k, &c16[i].v};
+        for (int j = 0; j < 3; ++j) {
+            const size_t bytes = align256(elems[j] * sizeof(f16));
+            if (off + bytes > ws_bytes) return hipErrorNotSupported;
+            total8 += (unsigned)(elems[j] / 8);
+            cv.src[cv.count] = reinterpret_cast<const float*>(src[j]);
+            cv.dst[cv.count] = reinterpret_cast<f16*>(ws + off);
+            cv.end8[cv.count] = total8;
+            ++cv.count;
+            *dstp[j] = ws + off;
+            off += bytes;
+        }
+    }
+    if (total8 > 0 && (phase_mask & 1)) {
+        hipLaunchKernelGGL(convert_f32_f16_kernel, dim3((total8 + 255) / 256), dim3(256), 0, stream, cv);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return launch_group_chunk(c16, n, InType::F16, out, nullptr, 0, stream, 0, 0, 0, phase_mask);
+}
+
 static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutType out, void* workspace,
                                      size_t ws_bytes, hipStream_t stream, int force_q_waves, int force_kv_waves,
                                      int force_splits, int phase_mask) {
+    if (in == InType::F32 && force_q_waves == 0 && force_kv_waves == 0 && force_splits == 0) {
+        const hipError_t e = launch_f32_via_f16(calls, n, out, workspace, ws_bytes, stream, phase_mask);
+        if (e != hipErrorNotSupported) return e;
+    }
     const GroupPlan p =
         plan_group(calls, n, workspace ? ws_bytes : 0, force_q_waves, force_kv_waves, force_splits, in);
     FwdArgs a{};
