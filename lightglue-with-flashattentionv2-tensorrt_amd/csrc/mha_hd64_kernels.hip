@@ -977,9 +977,14 @@ static bool direct_enabled() {
     return on;
 }
 
-// Tiles of 64 keys per wave of the single-pass kernel for this launch, or 0 if it does not apply:
-// fp16 input, every call's keys within 8 waves x 2 tiles, and at most 256 workgroups of 32 rows
-// (one residency round: the launches the ring kernel can only fill by splitting the keys).
+// Tiles of 64 keys per wave of the single-pass kernels for this launch, or 0 if they do not apply:
+// fp16 input, every call's keys within 8 waves x 2 tiles, and at most max_wgs workgroups of `rows`
+// query rows. 16-row blocks: at most 256 (one per CU, one round). 32-row blocks: at most 768 —
+// up to three rounds of 256 still beat the LDS ring's plans there (tools/batch_sweep.py, graph
+// replay, us per launch, 32-row kernel vs planner's ring plan: B=3 N=1024 10.3 vs 18.1, B=6 15.3 vs
+// 19.7, B=6 N=512 6.3 vs 9.5, B=12 N=512 8.7 vs 13.5; at 1024 blocks the ring wins: B=8 N=1024
+// 15.5 vs 21.0, B=16 N=512 10.4 vs 11.2).
+constexpr long kDirectMaxWgs16 = 256, kDirectMaxWgs32 = 768;
 static int direct_tiles_for(const Call* calls, int n, InType in, bool forced, int rows = 32) {
     if (in != InType::F16 || (!forced && !direct_enabled())) return 0;
     long wgs = 0;
@@ -989,7 +994,7 @@ static int direct_tiles_for(const Call* calls, int n, InType in, bool forced, in
         tiles = std::max(tiles, (calls[i].nkv + 8 * kTileKV - 1) / (8 * kTileKV));
         wgs += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + rows - 1) / rows);
     }
-    return (forced || wgs <= 256) ? tiles : 0;
+    return (forced || wgs <= (rows == 16 ? kDirectMaxWgs16 : kDirectMaxWgs32)) ? tiles : 0;
 }
 
 // The 16-row single-pass kernel first (default; MHA_HD64_DIRECT_ROWS=32 keeps 32-row blocks)

@@ -234,7 +234,9 @@ def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
 @pytest.mark.parametrize("batch,nq,nkv,code", [
     (1, 1024, 1024, 22),     # the metric call: 256 blocks of 16 rows, 1024 keys
     (1, 2048, 1024, 21),     # 512 16-row blocks, 256 of 32 rows: the 32-row kernel
-    (2, 2048, 1024, None),   # 512 32-row blocks: the ring kernel fills the chip by itself
+    (2, 2048, 1024, 21),     # 512 32-row blocks: two rounds of the 32-row kernel
+    (6, 1024, 1024, 21),     # 768: three rounds
+    (7, 1024, 1024, None),   # 896 32-row blocks: the LDS ring kernel
     (1, 1024, 1025, None),   # more keys than 8 waves x 2 tiles
     (1, 256, 256, 22),
     (1, 1, 1, 22),
@@ -244,7 +246,7 @@ def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
 ])
 def test_planner_single_pass_rule(lib, batch, nq, nkv, code):
     """Single-pass kernels iff fp16 and nkv <= 1024: plan code 22 (16-row blocks) when at most 256
-    of them, else 21 (32-row blocks) when at most 256 of those; they need no workspace and never
+    of them, else 21 (32-row blocks) when at most 768 of those; they need no workspace and never
     split."""
     out = (ctypes.c_int32 * 4)()
     need = lib.mha_hd64_plan(batch, 4, nq, nkv, 5242880, out)

@@ -1,0 +1,24 @@
+"""Diagnostic: per-launch graph-replay time of batched 1xBx4xNxN launches under the planner's
+default plan (code 0), the 32-row single-pass kernel (21) and the 16-row one (22).
+    python tools/batch_sweep.py [BxN ...]"""
+import json, os, sys
+REPO = "/root/repo" if os.path.exists("/root/repo") else os.getcwd()
+sys.path[:0] = [REPO, os.path.join(REPO, "lightglue-with-flashattentionv2-tensorrt_amd"), os.path.join(REPO, "tools")]
+import torch
+from lightglue_amd import _lib, synth
+from direct_check import per_launch_us
+lib = _lib.load()
+dev = torch.device("cuda:0")
+ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+res = {}
+cases = [tuple(int(x) for x in c.split("x")) for c in sys.argv[1:]] or [(8, 1024), (2, 1024), (4, 1024), (8, 512), (2, 512)]
+for batch, n in cases:
+    qn, kn, vn = synth.qkv(5, n, n, batch=batch)
+    q, k, v = (torch.from_numpy(x).to(dev).half().contiguous() for x in (qn, kn, vn))
+    o = torch.empty_like(q)
+    def run(code):
+        st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), batch, 4, n, n, 0, 0,
+                                        code, 0, 0, ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream, 3)
+        assert st == 0
+    res[f"b{batch}_n{n}"] = {str(c): round(per_launch_us(lambda: run(c)), 3) for c in (0, 21, 22)}
+print(json.dumps(res))
