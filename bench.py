@@ -238,12 +238,12 @@ def sweep(torch, lib, device, stream, nq, nkv):
     from lightglue_amd import synth
 
     ws_buf = torch.empty(256 << 20, dtype=torch.uint8, device=device)
-    for batch in (1, 2, 8):
+    for batch in [int(b) for b in os.environ.get("SWEEP_BATCHES", "1,2,8").split(",")]:
         qn, kn, vn = synth.qkv(7, nq, nkv, batch=batch)
         q, k, v = (torch.from_numpy(x).to(device).half().contiguous() for x in (qn, kn, vn))
         o = torch.empty_like(q)
-        for qw, kw in ((4, 1), (2, 2), (1, 2), (4, 2), (2, 4), (1, 8), (21, 0), (22, 0)):
-            for splits in ((0,) if qw >= 21 or kw >= 4 else (1, 2, 4, 8, 16)):
+        for qw, kw in ((0, 0), (4, 1), (2, 2), (1, 2), (4, 2), (2, 4), (1, 8), (21, 0), (22, 0)):
+            for splits in ((0,) if qw >= 21 or qw == 0 or kw >= 4 else (1, 2, 4, 8, 16)):
                 def run(mask=3):
                     return lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), batch,
                                                       4, nq, nkv, 0, 0, qw, kw, splits, ws_buf.data_ptr(),

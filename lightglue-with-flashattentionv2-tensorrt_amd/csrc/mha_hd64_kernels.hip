@@ -1047,8 +1047,17 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
         rb = 1;
         long blocks128 = 0;
         for (int i = 0; i < n; ++i) blocks128 += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 127) / 128);
-        if (blocks128 >= 256) {
-            qw = 4;  // enough 128-row query blocks to fill the chip: 8 waves, no cross-WG split
+        // (bench.py --sweep, profiles/r01/ring_plan_sweep.json; eager us per launch)
+        if (blocks128 > 256) {
+            // more than one round of 128-row blocks: 4 waves (48 KiB LDS, several workgroups per
+            // CU) beat (4,2)'s 8 (96 KiB, one per CU): 1024^2 B=16 29.3 vs 33.1, 2048^2 B=8 51.5
+            // vs 57.1, 1536^2 B=8 36.3 vs 40.8
+            qw = 4;
+            kw = 1;
+        } else if (blocks128 > 128) {
+            // one round of 128-row blocks: (4,2), no cross-WG split (1536^2 B=3 21.6 vs 29.0 for
+            // the (2,2) split plans, B=4 22.6 vs 29.8; 1024^2 B=8 18.8 vs 19.6 for (4,1))
+            qw = 4;
             kw = 2;
         } else {
             qw = 2;
@@ -1085,7 +1094,9 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
     long groups = 0;
     for (int i = 0; i < n; ++i)
         groups += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + block_m - 1) / block_m);
-    int want = force_splits > 0 ? force_splits : (int)std::max(1L, (256 + groups - 1) / std::max(1L, groups));
+    // splits: as many as keep the grid within one round of 256 workgroups (a second partial
+    // round costs more than the split saves: 1536^2 B=1 (2,2) 3-way 19.1 vs 2-way 13.9 us)
+    int want = force_splits > 0 ? force_splits : (int)std::max(1L, 256 / std::max(1L, groups));
     want = std::max(1, std::min(want, kMaxSplits));
     if (kw >= 4) {
         // single-super-tile shapes: every split must be exactly one super-tile (their LDS ring
