@@ -62,11 +62,15 @@ __device__ __forceinline__ void wait_vm() {
 
 // KW waves (key slices) per workgroup x TPW 64-key tiles per wave. (16 waves x 1 tile, four per
 // SIMD, measured 7.7 us against 6.3 us for 8 x 2 at 1x4x1024x1024.)
-template <typename TOut, int KW, int TPW, bool MULTI>
+// PASSES = 2 (nkv in (1024, 2048], 4 waves): each wave's 2·TPW tiles go through its TPW slots twice;
+// pass 1's K(TPW + t) is issued into slot t as soon as pass 0's PV has V(t)'s fragments in
+// registers, so the second pass's loads queue behind the first pass's without a gap.
+template <typename TOut, int KW, int TPW, bool MULTI, int PASSES = 1>
 __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) {
+    static_assert(PASSES == 1 || (PASSES == 2 && TPW * KW == 16), "two passes: 4 waves x 2 x 4 tiles or 8 x 2 x 2");
     constexpr int NT = 64 * KW;
     constexpr int BLOCK_M = 32;                         // query rows per workgroup
-    constexpr int WAVE_KEYS = kTileKV * TPW;            // keys per wave
+    constexpr int WAVE_KEYS = kTileKV * TPW * PASSES;   // keys per wave
     constexpr int OROW = 68;                            // epilogue fp32 row pitch (64 dims + 4 pad)
     constexpr int EPI_WAVE = BLOCK_M * OROW * 4;        // one wave's staged Oᵀ
     // Wave-private region: the wave's V tiles, later its staged Oᵀ (8704 = 68 x 128 B keeps the
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
     const int q_row = qtile * BLOCK_M + r;
     const int key0 = wave * WAVE_KEYS;
     // tiles of this wave holding at least one key (wave-uniform)
-    const int n_t = max(0, min(TPW, (nkv - key0 + kTileKV - 1) / kTileKV));
+    const int n_t = max(0, min(TPW * PASSES, (nkv - key0 + kTileKV - 1) / kTileKV));
     const unsigned region = (unsigned)wave * RS;
 
     f32x16 o0, o1;  // Oᵀ: dims 0..31 / 32..63, query on the lane
@@ -133,21 +137,28 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         const unsigned k_lane[2] = {lrow + (((lane & 7) ^ ((lane >> 4) & 7)) << 4),
                                     lrow + (((lane & 7) ^ ((4 + (lane >> 4)) & 7)) << 4)};
         const unsigned v_lane_off = lrow + (((lane & 7) ^ (((lane >> 4) & 1) << 2)) << 4);
-        auto dma_piece = [&](__amdgpu_buffer_rsrc_t rs, unsigned voff, int i) {
+        // piece i of the wave's key slice (source) into piece li of its region (li = i except in
+        // the second pass, whose tile TPW + t goes into slot t)
+        auto dma_piece = [&](__amdgpu_buffer_rsrc_t rs, unsigned voff, int i, int li) {
             if (MHA_ABL & ABL_NO_GLOAD) return;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * i),
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * li),
                                                      16, voff, 1024 * i, 0, 0);
         };
         auto dma_k = [&](int t0, int t1) {  // K of tiles [t0, t1) into their slots
 #pragma unroll
-            for (int i = 8 * t0; i < 8 * t1; ++i) dma_piece(k_rs, k_lane[i & 1], i);
+            for (int i = 8 * t0; i < 8 * t1; ++i) dma_piece(k_rs, k_lane[i & 1], i, i);
         };
-        auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, int t) {  // V of tile t into slot t
+        // K of tile TPW + t (second pass) into slot t; the swizzle repeats every 2 pieces
+        auto dma_k2 = [&](int t) {
 #pragma unroll
-            for (int i = 8 * t; i < 8 * t + 8; ++i) dma_piece(rs, v_lane_off, i);
+            for (int i = 0; i < 8; ++i) dma_piece(k_rs, k_lane[i & 1], 8 * (TPW + t) + i, 8 * t + i);
+        };
+        auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, int t, int slot) {  // V of tile t into `slot`
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dma_piece(rs, v_lane_off, 8 * t + i, 8 * slot + i);
         };
         // K fragments of tile t (A operand of Sᵀ = K·Qᵀ): kf[2s] = K[64t+r][16s+8hh..+7], kf[2s+1] = rows +32
-        auto read_k = [&](int t, f16x8(&kf)[8]) {
+        auto read_k = [&](int t, f16x8(&kf)[8]) {  // t: the slot
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -220,38 +231,56 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         f16x8 p[TPW][2][2];  // P (fp16) as the B operand: p[t][half][k-step]
         f32x16 sc[TPW][2];   // scores of tiles 1.. (log2 units, against the first tile's max)
         // Oᵀ += Vᵀ·Pᵀ for tile t and the row sums, once V(t) has landed (V(t+1..) may be in flight)
-        auto pv = [&](int t, bool waited = false) {
-            if (!waited) switch (TPW - 1 - t) {
+        // Oᵀ += Vᵀ·Pᵀ for the tile in slot t (probabilities pt) and the row sums, once its V has
+        // landed: `younger` = DMA groups of 8 issued after it (-1: already waited). first: the
+        // accumulators start from an inline 0. refill: K of tile TPW + t is issued into slot t as
+        // soon as V's fragments are in registers (the two-pass form's first pass).
+        auto pv = [&](int t, const f16x8(&pt)[2][2], int younger, bool first, bool refill) {
+            switch (younger) {
+                case -1: break;
                 case 0: wait_vm<0>(); break;
                 case 1: wait_vm<8>(); break;
                 case 2: wait_vm<16>(); break;
                 default: wait_vm<24>(); break;
             }
-            if (t == 0) DSTAMP(3);
+            if (first) DSTAMP(3);
             const unsigned va0 = region + t * kTileBytes + v_lane + 64 * vb;
             const unsigned va1 = region + t * kTileBytes + v_lane + 64 * (1 - vb);
+            f16x8 vfa[2][2], vfb[2][2];
+            auto read_v = [&](int jj, int ss) {
+                const unsigned rowc = 128 * (32 * jj + 16 * ss);
+                vfa[jj][ss] = cat8(tr_read(lds, va0 + rowc), tr_read(lds, va0 + rowc + 8 * 128));
+                vfb[jj][ss] = cat8(tr_read(lds, va1 + rowc), tr_read(lds, va1 + rowc + 8 * 128));
+            };
+            if (refill) {  // every fragment in registers before the slot is refilled
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+                    for (int ss = 0; ss < 2; ++ss) read_v(jj, ss);
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(vfa[0][0]), "+v"(vfa[0][1]), "+v"(vfa[1][0]), "+v"(vfa[1][1]), "+v"(vfb[0][0]),
+                               "+v"(vfb[0][1]), "+v"(vfb[1][0]), "+v"(vfb[1][1])::"memory");
+                dma_k2(t);
+            }
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
                 for (int ss = 0; ss < 2; ++ss) {
-                    const unsigned rowc = 128 * (32 * jj + 16 * ss);
-                    const f16x8 vfa = cat8(tr_read(lds, va0 + rowc), tr_read(lds, va0 + rowc + 8 * 128));
-                    const f16x8 vfb = cat8(tr_read(lds, va1 + rowc), tr_read(lds, va1 + rowc + 8 * 128));
+                    if (!refill) read_v(jj, ss);
                     if (MHA_ABL & ABL_NO_PV) {
-                        keep_live(vfa);
-                        keep_live(vfb);
-                        keep_live(p[t][jj][ss]);
-                        if (t == 0 && jj == 0 && ss == 0) {
+                        keep_live(vfa[jj][ss]);
+                        keep_live(vfb[jj][ss]);
+                        keep_live(pt[jj][ss]);
+                        if (first && jj == 0 && ss == 0) {
                             o0 = o1 = f32x16{};
                             l_acc = f32x4{0.f, 0.f, 0.f, 0.f};
                         }
                         continue;
                     }
-                    const bool first = t == 0 && jj == 0 && ss == 0;  // accumulators start at inline 0
-                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa, p[t][jj][ss], first ? f32x16{} : o0, 0, 0, 0);
-                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb, p[t][jj][ss], first ? f32x16{} : o1, 0, 0, 0);
-                    l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, p[t][jj][ss], first ? f32x4{} : l_acc, 0,
-                                                                   0, 0);
+                    const bool z = first && jj == 0 && ss == 0;  // accumulators start at inline 0
+                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa[jj][ss], pt[jj][ss], z ? f32x16{} : o0, 0, 0, 0);
+                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb[jj][ss], pt[jj][ss], z ? f32x16{} : o1, 0, 0, 0);
+                    l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, pt[jj][ss], z ? f32x4{} : l_acc, 0, 0, 0);
                 }
         };
         auto exp_pack = [&](f32x16 c0, f32x16 c1, f16x8(&pt)[2][2]) {
@@ -278,7 +307,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
             // K(t)'s fragments are in registers before V(t)'s DMA overwrites slot t
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]), "+v"(kf[4]),
                          "+v"(kf[5]), "+v"(kf[6]), "+v"(kf[7])::"memory");
-            dma_tile(v_rs, t);
+            dma_tile(v_rs, t, t);
             // Sᵀ = K·Qᵀ - m, two 32-key halves. The bias k-step (-m and the tail mask) runs first,
             // except on a full first tile: there it runs last, once the tile's max is known, so the
             // scores need no subtraction (an MFMA instead of 32 VALU ops).
@@ -353,16 +382,73 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
                 }
                 m_run += d;
             }
-            pv(0);  // tile 0's PV on the matrix pipe beside the later tiles' exponentials (one block)
+            // tile 0's PV on the matrix pipe beside the later tiles' exponentials (one block)
+            pv(0, p[0], TPW - 1, true, PASSES > 1);
 #pragma unroll
             for (int t = 1; t < TPW; ++t) exp_pack(sc[t][0], sc[t][1], p[t]);
         }
         DSTAMP(2);
-        // Phase 2: the remaining tiles' Oᵀ += Vᵀ·Pᵀ (tile 0's ran beside the exponentials). Every V
-        // has long landed by now: one wait, so the compiler may hoist later tiles' fragment reads.
-        if constexpr (TPW > 1) wait_vm<0>();
+        if constexpr (PASSES == 1) {
+            // Phase 2: the remaining tiles' Oᵀ += Vᵀ·Pᵀ (tile 0's ran beside the exponentials). Every
+            // V has long landed by now: one wait, so the compiler may hoist later fragment reads.
+            if constexpr (TPW > 1) wait_vm<0>();
 #pragma unroll
-        for (int t = (TPW > 1 ? 1 : 0); t < TPW; ++t) pv(t, TPW > 1);
+            for (int t = (TPW > 1 ? 1 : 0); t < TPW; ++t) pv(t, p[t], TPW > 1 ? -1 : 0, TPW == 1, false);
+        } else {
+            // First pass's remaining PVs, each refilling its slot with the second pass's K: younger
+            // than V(t) are V(t+1..) and K(TPW..TPW+t-1), always TPW - 1 groups.
+#pragma unroll
+            for (int t = 1; t < TPW; ++t) pv(t, p[t], TPW - 1, false, true);
+            // Second pass: tiles TPW + t through slot t, scored against the running max (bias k-step
+            // first), ONE rescale decision for the pass (rescaling O and the row sums), exponentials,
+            // then PV as each V lands.
+            set_bias();
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                f16x8 kf[8];
+                wait_vm<8 * (TPW - 1)>();  // K(TPW+t) landed: younger are K(TPW+t+1..), V(TPW..TPW+t-1)
+                read_k(t, kf);
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]), "+v"(kf[4]),
+                             "+v"(kf[5]), "+v"(kf[6]), "+v"(kf[7])::"memory");
+                dma_tile(v_rs, TPW + t, t);
+                const bool partial = key0 + kTileKV * (TPW + t + 1) > nkv;  // wave-uniform
+                const f16x8 a_plain = f16x8{one_h, one_h, 0, 0, 0, 0, 0, 0};
+                const f16x8 ab0 = partial ? a_bias_of(TPW + t, 0) : a_plain;
+                const f16x8 ab1 = partial ? a_bias_of(TPW + t, 1) : a_plain;
+                f32x16 c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab0, b_bias, f32x16{}, 0, 0, 0);
+                f32x16 c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab1, b_bias, f32x16{}, 0, 0, 0);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s], qf[s], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s + 1], qf[s], c1, 0, 0, 0);
+                }
+                sc[t][0] = c0;
+                sc[t][1] = c1;
+            }
+            {
+                float mx = -INFINITY;
+#pragma unroll
+                for (int t = 0; t < TPW; ++t) mx = fmaxf(mx, tree_max(sc[t][0], sc[t][1]));
+                mx = xhalf_max(mx);
+                if (__builtin_amdgcn_ballot_w64(mx > kRescaleThr) != 0) {
+                    const float d = fmaxf(mx, 0.f);
+                    const float alpha = __builtin_amdgcn_exp2f(-d);
+                    o0 *= alpha;
+                    o1 *= alpha;
+                    l_acc *= alpha;
+#pragma unroll
+                    for (int t = 0; t < TPW; ++t) {
+                        sc[t][0] -= d;
+                        sc[t][1] -= d;
+                    }
+                    m_run += d;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) exp_pack(sc[t][0], sc[t][1], p[t]);
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) pv(t, p[t], TPW - 1 - t, false, false);
+        }
     }
 
     DSTAMP(4);
@@ -420,12 +506,13 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
 #endif
 }
 
-template <typename TOut, int KW, int TPW>
+template <typename TOut, int KW, int TPW, int PASSES = 1>
 hipError_t launch_direct_t(const FwdArgs& a, int grid, hipStream_t stream) {
     if (a.n_calls > 1)
-        hipLaunchKernelGGL((mha_hd64_direct_kernel<TOut, KW, TPW, true>), dim3(grid), dim3(64 * KW), 0, stream, a);
+        hipLaunchKernelGGL((mha_hd64_direct_kernel<TOut, KW, TPW, true, PASSES>), dim3(grid), dim3(64 * KW), 0, stream, a);
     else
-        hipLaunchKernelGGL((mha_hd64_direct_kernel<TOut, KW, TPW, false>), dim3(grid), dim3(64 * KW), 0, stream, a);
+        hipLaunchKernelGGL((mha_hd64_direct_kernel<TOut, KW, TPW, false, PASSES>), dim3(grid), dim3(64 * KW), 0, stream,
+                           a);
     return hipGetLastError();
 }
 
@@ -438,6 +525,13 @@ hipError_t launch_direct(const FwdArgs& a, int grid, int tiles_per_wave, bool ou
         const char* e = std::getenv("MHA_HD64_DIRECT_WAVES");
         return !(e && e[0] == '8');
     }();
+    // nkv in (1024, 2048] (tiles_per_wave 3, 4): two passes, 4 waves x 2 x 4 tiles (or 8 x 2 x 2)
+    if (tiles_per_wave > 2) {
+        if (four)
+            return out_f32 ? launch_direct_t<float, 4, 4, 2>(a, grid, stream)
+                           : launch_direct_t<f16, 4, 4, 2>(a, grid, stream);
+        return out_f32 ? launch_direct_t<float, 8, 2, 2>(a, grid, stream) : launch_direct_t<f16, 8, 2, 2>(a, grid, stream);
+    }
     switch ((four ? 100 : 0) + tiles_per_wave * 2 + (out_f32 ? 1 : 0)) {
         case 2: return launch_direct_t<f16, 8, 1>(a, grid, stream);
         case 3: return launch_direct_t<float, 8, 1>(a, grid, stream);

@@ -978,7 +978,7 @@ static bool direct_enabled() {
 }
 
 // Tiles of 64 keys per wave of the single-pass kernels for this launch, or 0 if they do not apply:
-// fp16 input, every call's keys within 8 waves x 2 tiles, and at most max_wgs workgroups of `rows`
+// fp16 input, every call's keys within 8 waves x 2 tiles (x 2 passes for 32-row blocks), and at most max_wgs workgroups of `rows`
 // query rows. 16-row blocks: at most 256 (one per CU, one round). 32-row blocks: at most 768 —
 // up to three rounds of 256 still beat the LDS ring's plans there (tools/batch_sweep.py, graph
 // replay, us per launch, 32-row kernel vs planner's ring plan: B=3 N=1024 10.3 vs 18.1, B=6 15.3 vs
@@ -989,12 +989,22 @@ static int direct_tiles_for(const Call* calls, int n, InType in, bool forced, in
     if (in != InType::F16 || (!forced && !direct_enabled())) return 0;
     long wgs = 0;
     int tiles = 1;
+    // keys per call: <= 1024 for 16-row blocks; <= 2048 for 32-row blocks (tiles 3, 4: the
+    // two-pass form, 4 waves x 2 x 4 tiles)
+    const int max_tiles = rows == 16 ? 2 : 4;
     for (int i = 0; i < n; ++i) {
-        if (calls[i].nkv > 8 * 2 * kTileKV) return 0;
+        if (calls[i].nkv > 8 * max_tiles * kTileKV) return 0;
         tiles = std::max(tiles, (calls[i].nkv + 8 * kTileKV - 1) / (8 * kTileKV));
         wgs += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + rows - 1) / rows);
     }
-    return (forced || wgs <= (rows == 16 ? kDirectMaxWgs16 : kDirectMaxWgs32)) ? tiles : 0;
+    // two-pass form (tiles 3, 4): 96..256 workgroups — from 512 on, and at 64, the ring's plans win
+    // (tools/batch_sweep.py, us per launch, two-pass kernel vs ring plan: 2048^2 B=1 9.87 vs 13.04,
+    // B=2 17.6 vs 17.3, B=3 24.8 vs 22.4; 1536^2 B=1 8.13 vs 11.12, B=2 15.3 vs 13.4; Nq x Nkv
+    // 1024x2048 8.64 vs 10.74, 768x2048 8.39 vs 10.24, B=2 1024x2048 9.22 vs 13.10, 512x2048
+    // 8.35 vs 7.95)
+    if (tiles > 2 && rows == 32 && !forced && (wgs < 96 || wgs > 256)) return 0;
+    const long max_wgs = rows == 16 ? kDirectMaxWgs16 : kDirectMaxWgs32;
+    return (forced || wgs <= max_wgs) ? tiles : 0;
 }
 
 // The 16-row single-pass kernel first (default; MHA_HD64_DIRECT_ROWS=32 keeps 32-row blocks)

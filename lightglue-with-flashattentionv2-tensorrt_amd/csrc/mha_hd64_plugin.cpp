@@ -381,8 +381,9 @@ int32_t mha_hd64_launch_forced(const void* q, const void* k, const void* v, void
     const bool fell_back = single_tile && plan_qw == 2 && plan.kv_waves == 2;
     // q_waves = 21 / 22 force the 32- / 16-row single-pass kernel (kv_waves / splits ignored)
     const bool direct = q_waves == mha_hd64::kForceDirect || q_waves == mha_hd64::kForceDirect16;
-    if (direct && plan.direct_tiles == 0)
-        return fail(MHA_HD64_STATUS_BAD_PARAM, __FILE__, __LINE__, "single-pass kernel: fp16 input, nkv <= 1024");
+    if (direct && plan_qw != q_waves)
+        return fail(MHA_HD64_STATUS_BAD_PARAM, __FILE__, __LINE__,
+                    "single-pass kernel: fp16 input, nkv <= 1024 (16-row) / 2048 (32-row)");
     if (q_waves != 0 && !direct && !fell_back && (plan_qw != q_waves || plan.kv_waves != kv_waves))
         return fail(MHA_HD64_STATUS_BAD_PARAM, __FILE__, __LINE__, "forced workgroup shape is not compiled");
     if (splits > 1 && !single_tile && !direct && plan.splits != splits)

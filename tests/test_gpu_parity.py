@@ -496,6 +496,54 @@ def test_direct_kernel_matches_oracle(nq, nkv, code, dev, oracle_mod):
         assert _maxdiff(got[:, :, rows], ref) <= tol
 
 
+# nkv in (1024, 2048]: the 32-row kernel's two-pass form (4 waves x 2 x 4 tiles through 4 slots)
+DIRECT2_SHAPES = [(2048, 2048), (1000, 1500), (64, 2048), (300, 1025), (17, 1900), (1024, 1100), (513, 1537)]
+
+
+@pytest.mark.parametrize("nq,nkv", DIRECT2_SHAPES)
+def test_direct_kernel_two_pass_matches_oracle(nq, nkv, dev, oracle_mod):
+    """Second-pass tiles partial or wholly past nkv, waves without keys, both output types."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    qn, kn, vn = synth.qkv(91 + nq + 5 * nkv, nq, nkv)
+    q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
+    rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 48)), nq - 1])
+    ref = oracle_mod.attention_c(np.ascontiguousarray(q16[:, :, rows]), k16, v16)
+    q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
+        o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
+        _forced(lib, q, k, v, o, nq, nkv, 21, 0, 0, ws)
+        assert lib.mha_hd64_last_combine_form() == 0
+        torch.cuda.synchronize()
+        got = o.float().cpu().numpy()
+        assert np.isfinite(got).all(), "unwritten or NaN output rows"
+        assert _maxdiff(got[:, :, rows], ref) <= tol
+
+
+def test_direct_kernel_two_pass_rescale(dev, oracle_mod):
+    """Spikes in the second pass's tiles move the running max after the first pass's PV (O and
+    the row sums rescaled): key 300 (wave 0, pass 1), key 1900 (wave 3, pass 1), key 10 (pass 0,
+    small gain: no move), and nkv = 1100 (wave 2 partial, wave 3 empty)."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    nq = 256
+    for nkv, krow, gain in ((2048, 300, 6.0), (2048, 1900, 3.0), (1100, 1090, 6.0), (2048, 10, 0.5)):
+        qn, kn, vn = synth.qkv(707 + nkv + krow, nq, nkv)
+        kn = synth.spike(qn, kn, 5, krow, gain)
+        q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
+        ref = oracle_mod.attention_c(q16, k16, v16)
+        q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+        for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
+            o = torch.empty(q.shape, dtype=out_dt, device=dev)
+            _forced(lib, q, k, v, o, nq, nkv, 21, 0, 0, ws)
+            torch.cuda.synchronize()
+            assert _maxdiff(o.float().cpu().numpy(), ref) <= tol, (nkv, krow, gain, out_dt)
+
+
 def test_direct_kernel_rescale_and_masked_waves(dev, oracle_mod):
     """A spike in a wave's second tile forces the rescale of the first tile's probabilities (key
     100: wave 0, tile 1; key 1000: wave 7, tile 1); nkv = 600 leaves waves 5-7 without keys."""
@@ -546,11 +594,12 @@ def test_direct_kernel_forced_outside_its_range_is_rejected(dev):
 
     lib = _lib.load()
     ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
-    for nkv, dt in ((1025, torch.float16), (512, torch.float32)):
+    for nkv, dt, codes in ((1025, torch.float16, (22,)), (2049, torch.float16, (21, 22)),
+                           (512, torch.float32, (21, 22))):
         q = torch.zeros(1, 4, 64, 64, dtype=dt, device=dev)
         k = torch.zeros(1, 4, nkv, 64, dtype=dt, device=dev)
         o = torch.empty_like(q)
-        for code in (21, 22):
+        for code in codes:
             st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), k.data_ptr(), o.data_ptr(), 1, 4, 64, nkv,
                                             int(dt == torch.float32), int(dt == torch.float32), code, 0, 0,
                                             ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream, 3)

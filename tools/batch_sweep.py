@@ -11,14 +11,23 @@ lib = _lib.load()
 dev = torch.device("cuda:0")
 ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
 res = {}
+# cases: BxN (Nq = Nkv = N) or BxNQxNKV
 cases = [tuple(int(x) for x in c.split("x")) for c in sys.argv[1:]] or [(8, 1024), (2, 1024), (4, 1024), (8, 512), (2, 512)]
-for batch, n in cases:
-    qn, kn, vn = synth.qkv(5, n, n, batch=batch)
+for case in cases:
+    batch, n = case[0], case[1]
+    nkv = case[2] if len(case) > 2 else n
+    qn, kn, vn = synth.qkv(5, n, nkv, batch=batch)
     q, k, v = (torch.from_numpy(x).to(dev).half().contiguous() for x in (qn, kn, vn))
     o = torch.empty_like(q)
     def run(code):
-        st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), batch, 4, n, n, 0, 0,
+        st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), batch, 4, n, nkv, 0, 0,
                                         code, 0, 0, ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream, 3)
         assert st == 0
-    res[f"b{batch}_n{n}"] = {str(c): round(per_launch_us(lambda: run(c)), 3) for c in (0, 21, 22)}
+    row = {}
+    for c in (0, 21, 22):
+        try:
+            row[str(c)] = round(per_launch_us(lambda: run(c)), 3)
+        except AssertionError:  # plan not applicable to this shape
+            row[str(c)] = None
+    res[f"b{batch}_n{n}" + (f"x{nkv}" if nkv != n else "")] = row
 print(json.dumps(res))
