@@ -545,7 +545,7 @@ def main():
 
     if args.sweep and rank == 0:
         sweep(torch, lib, device, stream, nq, nkv)
-    if rank == 0 and not args.no_cpu_baseline and not args.quick:
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and not args.quick:  # CPU baseline: N=1 only
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, nq, nkv)
     if rank == 0:
         print(json.dumps(result), flush=True)
