@@ -79,7 +79,10 @@ __device__ __forceinline__ float max16(const f32x4 (&c)[4]) {
     return fmaxf(fmaxf(t[0], t[1]), fmaxf(t[2], t[3]));
 }
 
-template <typename TOut, int KW, int TPW, bool MULTI>
+// PASSES = 2 (nkv in (1024, 2048], 4 waves): each wave's 2·TPW tiles go through its TPW slots twice,
+// as in mha_hd64_direct.hip's two-pass form (pass 1's K(TPW + t) refills slot t once pass 0's PV
+// has V(t)'s fragments in registers).
+template <typename TOut, int KW, int TPW, bool MULTI, int PASSES = 1>
 // The single call's own arguments come first as plain scalars (q0 .. qtiles0: 12 dwords), so the
 // command processor can preload them into SGPRs (-amdgpu-kernarg-preload-count, Makefile) and the
 // first loads need no dependent kernarg fetch; grouped launches (MULTI) read the table `a`.
@@ -87,8 +90,9 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
                                                                         void* o0, int total_blocks, int nq0, int nkv0,
                                                                         int qtiles0, FwdArgs a) {
     static_assert(TPW >= 2 && TPW <= 4 && (KW == 4 || KW == 8), "waves x tiles per wave");
+    static_assert(PASSES == 1 || (PASSES == 2 && TPW == 4 && KW == 4), "two passes: 4 waves x 2 x 4 tiles");
     constexpr int BLOCK_M = 16;                     // query rows per workgroup
-    constexpr int WAVE_KEYS = kTileKV * TPW;
+    constexpr int WAVE_KEYS = kTileKV * TPW * PASSES;
     constexpr int OROW = 68;                        // epilogue fp32 row pitch
     constexpr int EPI_WAVE = BLOCK_M * OROW * 4;
     constexpr int RS = TPW * kTileBytes > EPI_WAVE ? TPW * kTileBytes : EPI_WAVE;
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
     const __amdgpu_buffer_rsrc_t v_rs = make_rsrc(Vb, (unsigned)nkv * kHeadDim * 2);
     const int q_row = qtile * BLOCK_M + i16;
     const int key0 = wave * WAVE_KEYS;
-    const int n_t = max(0, min(TPW, (nkv - key0 + kTileKV - 1) / kTileKV));
+    const int n_t = max(0, min(TPW * PASSES, (nkv - key0 + kTileKV - 1) / kTileKV));
     const unsigned region = (unsigned)wave * RS;
 
     f32x4 o[4];  // Oᵀ: dims 16db + 4g + j of query i16
@@ -161,17 +165,22 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         const unsigned k_lane[2] = {lrow + (((lane & 7) ^ ((lane >> 4) & 7)) << 4),
                                     lrow + (((lane & 7) ^ ((4 + (lane >> 4)) & 7)) << 4)};
         const unsigned v_lane_off = lrow + (((lane & 7) ^ (((lane >> 4) & 3) << 1)) << 4);
-        auto dma_piece = [&](__amdgpu_buffer_rsrc_t rs, unsigned voff, int i) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * i),
+        // source piece i of the wave's key slice into region piece li (li = i except in pass 1)
+        auto dma_piece = [&](__amdgpu_buffer_rsrc_t rs, unsigned voff, int i, int li) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * li),
                                                      16, voff, 1024 * i, 0, 0);
         };
         auto dma_k = [&](int t0, int t1) {
 #pragma unroll
-            for (int i = 8 * t0; i < 8 * t1; ++i) dma_piece(k_rs, k_lane[i & 1], i);
+            for (int i = 8 * t0; i < 8 * t1; ++i) dma_piece(k_rs, k_lane[i & 1], i, i);
         };
-        auto dma_v = [&](int t) {
+        auto dma_k2 = [&](int t) {  // K of tile TPW + t into slot t (the swizzle repeats every 2 pieces)
 #pragma unroll
-            for (int i = 8 * t; i < 8 * t + 8; ++i) dma_piece(v_rs, v_lane_off, i);
+            for (int i = 0; i < 8; ++i) dma_piece(k_rs, k_lane[i & 1], 8 * (TPW + t) + i, 8 * t + i);
+        };
+        auto dma_v = [&](int t, int slot) {  // V of tile t into `slot`
+#pragma unroll
+            for (int i = 0; i < 8; ++i) dma_piece(v_rs, v_lane_off, 8 * t + i, 8 * slot + i);
         };
         // K fragments of tile t (A operand of Sᵀ = K·Qᵀ): kf[kb][s] = K[64t+16kb+i16][32s+8g..+7]
         auto read_k = [&](int t, f16x8(&kf)[4][2]) {
@@ -221,17 +230,33 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
 
         f16x8 p[TPW][2];   // P (fp16), B operand of step u of tile t
         f32x4 sc[TPW][4];  // raw scores of tiles 1..
-        auto pv = [&](int t) {
+        // Oᵀ += Vᵀ·Pᵀ for the tile in slot t; first: accumulators from an inline 0; refill: V's
+        // fragments all in registers, then K of tile TPW + t into slot t, then the MFMAs
+        auto pv = [&](int t, bool first, bool refill) {
+            f16x8 va[2][4];
+            auto read_v = [&](int u, int db) {
+                const unsigned off = (unsigned)(t * kTileBytes + 128 * 32 * u);
+                va[u][db] = cat8(tr_read(lds, vbase[db] + off), tr_read(lds, vbase[db] + off + 16 * 128));
+            };
+            if (refill) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+#pragma unroll
+                    for (int db = 0; db < 4; ++db) read_v(u, db);
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(va[0][0]), "+v"(va[0][1]), "+v"(va[0][2]), "+v"(va[0][3]), "+v"(va[1][0]),
+                               "+v"(va[1][1]), "+v"(va[1][2]), "+v"(va[1][3])::"memory");
+                dma_k2(t);
+            }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                const unsigned off = (unsigned)(t * kTileBytes + 128 * 32 * u);
 #pragma unroll
                 for (int db = 0; db < 4; ++db) {
-                    const f16x8 va = cat8(tr_read(lds, vbase[db] + off), tr_read(lds, vbase[db] + off + 16 * 128));
-                    const bool first = t == 0 && u == 0;
-                    o[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, p[t][u], first ? f32x4{} : o[db], 0, 0, 0);
+                    if (!refill) read_v(u, db);
+                    const bool z = first && u == 0;
+                    o[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[u][db], p[t][u], z ? f32x4{} : o[db], 0, 0, 0);
                 }
-                l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, p[t][u], (t == 0 && u == 0) ? f32x4{} : l_acc, 0,
+                l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, p[t][u], (first && u == 0) ? f32x4{} : l_acc, 0,
                                                                0, 0);
             }
         };
@@ -255,7 +280,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
             asm volatile("s_waitcnt lgkmcnt(0)"
                          : "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[1][0]), "+v"(kf[1][1]), "+v"(kf[2][0]),
                            "+v"(kf[2][1]), "+v"(kf[3][0]), "+v"(kf[3][1])::"memory");
-            dma_v(t);  // over slot t, whose K is in registers
+            dma_v(t, t);  // over slot t, whose K is in registers
             f32x4 c[4];
 #pragma unroll
             for (int kb = 0; kb < 4; ++kb) {
@@ -295,13 +320,76 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         }
         wait_vmc<8 * (TPW - 1)>();  // V(0) landed
         DSTAMP(3);
-        pv(0);                      // beside the later tiles' exponentials
+        pv(0, true, PASSES > 1);    // beside the later tiles' exponentials
 #pragma unroll
         for (int t = 1; t < TPW; ++t) exp_pack(sc[t], p[t], m_run);
         DSTAMP(2);
-        wait_vmc<0>();
+        if constexpr (PASSES == 1) {
+            wait_vmc<0>();
 #pragma unroll
-        for (int t = 1; t < TPW; ++t) pv(t);
+            for (int t = 1; t < TPW; ++t) pv(t, false, false);
+        } else {
+            // pass 0's remaining PVs, each refilling its slot: younger than V(t) are V(t+1..) and
+            // K(TPW..TPW+t-1), always TPW - 1 groups of 8
+#pragma unroll
+            for (int t = 1; t < TPW; ++t) {
+                wait_vmc<8 * (TPW - 1)>();
+                pv(t, false, true);
+            }
+            // pass 1: tiles TPW + t through slot t, raw scores; ONE rescale decision for the pass
+            // (O and the row sums rescaled), then exponentials against the running max and PV
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                f16x8 kf[4][2];
+                wait_vmc<8 * (TPW - 1)>();  // K(TPW+t): younger are K(TPW+t+1..), V(TPW..TPW+t-1)
+                read_k(t, kf);
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[1][0]), "+v"(kf[1][1]), "+v"(kf[2][0]),
+                               "+v"(kf[2][1]), "+v"(kf[3][0]), "+v"(kf[3][1])::"memory");
+                dma_v(TPW + t, t);
+                f32x4 c[4];
+#pragma unroll
+                for (int kb = 0; kb < 4; ++kb) {
+                    c[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kb][0], qf[0], f32x4{}, 0, 0, 0);
+                    c[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kb][1], qf[1], c[kb], 0, 0, 0);
+                }
+                if (key0 + kTileKV * (TPW + t + 1) > nkv) {  // wave-uniform: mask keys past nkv
+#pragma unroll
+                    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (key0 + kTileKV * (TPW + t) + 16 * kb + 4 * g + e >= nkv) c[kb][e] = -INFINITY;
+                }
+#pragma unroll
+                for (int kb = 0; kb < 4; ++kb) sc[t][kb] = c[kb];
+            }
+            {
+                float mx = -INFINITY;
+#pragma unroll
+                for (int t = 0; t < TPW; ++t) mx = fmaxf(mx, max16(sc[t]));
+                const float ex = xquad_max(mx) - m_run;
+                if (__builtin_amdgcn_ballot_w64(ex > kRescaleThr) != 0) {
+                    const float d = fmaxf(ex, 0.f);
+                    const float alpha = __builtin_amdgcn_exp2f(-d);
+#pragma unroll
+                    for (int db = 0; db < 4; ++db) o[db] *= alpha;
+                    l_acc *= alpha;
+                    m_run += d;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) exp_pack(sc[t], p[t], m_run);
+#pragma unroll
+            for (int t = 0; t < TPW; ++t) {
+                switch (TPW - 1 - t) {  // V(TPW+t): younger are V(TPW+t+1..)
+                    case 0: wait_vmc<0>(); break;
+                    case 1: wait_vmc<8>(); break;
+                    case 2: wait_vmc<16>(); break;
+                    default: wait_vmc<24>(); break;
+                }
+                pv(t, false, false);
+            }
+        }
     }
     DSTAMP(4);
 
@@ -348,13 +436,13 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
 #endif
 }
 
-template <typename TOut, int KW, int TPW>
+template <typename TOut, int KW, int TPW, int PASSES = 1>
 hipError_t launch16_t(const FwdArgs& a, int grid, hipStream_t stream) {
     if (a.n_calls > 1)
-        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, true>), dim3(grid), dim3(64 * KW), 0, stream,
+        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, true, PASSES>), dim3(grid), dim3(64 * KW), 0, stream,
                            nullptr, nullptr, nullptr, nullptr, a.total_blocks, 0, 0, 0, a);
     else
-        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, false>), dim3(grid), dim3(64 * KW), 0, stream,
+        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, false, PASSES>), dim3(grid), dim3(64 * KW), 0, stream,
                            a.c[0].q, a.c[0].k, a.c[0].v, a.c[0].o, a.total_blocks, a.c[0].nq, a.c[0].nkv,
                            a.c[0].qtiles, a);
     return hipGetLastError();
@@ -365,6 +453,8 @@ hipError_t launch16_t(const FwdArgs& a, int grid, hipStream_t stream) {
 hipError_t launch_direct16(const FwdArgs& a, int grid, int tiles_per_wave, bool out_f32, hipStream_t stream) {
     // tiles_per_wave counts 64-key tiles per wave of the 8-wave form (1: nkv <= 512, 2: <= 1024);
     // 4 waves take twice as many
+    if (tiles_per_wave > 2)  // nkv in (1024, 2048]: 4 waves x two passes of 4 tiles
+        return out_f32 ? launch16_t<float, 4, 4, 2>(a, grid, stream) : launch16_t<f16, 4, 4, 2>(a, grid, stream);
     switch (tiles_per_wave * 2 + (out_f32 ? 1 : 0)) {
         case 2: return launch16_t<f16, 4, 2>(a, grid, stream);
         case 3: return launch16_t<float, 4, 2>(a, grid, stream);

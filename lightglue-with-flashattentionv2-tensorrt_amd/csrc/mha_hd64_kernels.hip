@@ -989,20 +989,19 @@ static int direct_tiles_for(const Call* calls, int n, InType in, bool forced, in
     if (in != InType::F16 || (!forced && !direct_enabled())) return 0;
     long wgs = 0;
     int tiles = 1;
-    // keys per call: <= 1024 for 16-row blocks; <= 2048 for 32-row blocks (tiles 3, 4: the
-    // two-pass form, 4 waves x 2 x 4 tiles)
-    const int max_tiles = rows == 16 ? 2 : 4;
+    // keys per call: <= 2048 (tiles 3, 4: the two-pass forms, 4 waves x 2 x 4 tiles)
+    const int max_tiles = 4;
     for (int i = 0; i < n; ++i) {
         if (calls[i].nkv > 8 * max_tiles * kTileKV) return 0;
         tiles = std::max(tiles, (calls[i].nkv + 8 * kTileKV - 1) / (8 * kTileKV));
         wgs += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + rows - 1) / rows);
     }
-    // two-pass form (tiles 3, 4): 96..256 workgroups — from 512 on, and at 64, the ring's plans win
-    // (tools/batch_sweep.py, us per launch, two-pass kernel vs ring plan: 2048^2 B=1 9.87 vs 13.04,
-    // B=2 17.6 vs 17.3, B=3 24.8 vs 22.4; 1536^2 B=1 8.13 vs 11.12, B=2 15.3 vs 13.4; Nq x Nkv
-    // 1024x2048 8.64 vs 10.74, 768x2048 8.39 vs 10.24, B=2 1024x2048 9.22 vs 13.10, 512x2048
-    // 8.35 vs 7.95)
-    if (tiles > 2 && rows == 32 && !forced && (wgs < 96 || wgs > 256)) return 0;
+    // two-pass forms (tiles 3, 4): one round only — from 512 workgroups on the ring's plans win;
+    // 32-row blocks from 96 on (tools/batch_sweep.py, us per launch, two-pass 16-row / 32-row
+    // kernel vs ring plan: 2048^2 B=1 - / 9.87 vs 13.04, B=2 - / 17.6 vs 17.3; 1536^2 B=1 - / 8.13
+    // vs 11.12; Nq x Nkv 1024x2048 7.40 / 8.57 vs 10.74, 768x2048 6.79 / 8.38 vs 10.24,
+    // 512x2048 6.68 / 8.33 vs 7.95, 256x2048 6.61 / 8.31 vs 7.69, 1024x1536 6.32 / 8.05 vs 9.84)
+    if (tiles > 2 && !forced && (wgs > 256 || (rows == 32 && wgs < 96))) return 0;
     const long max_wgs = rows == 16 ? kDirectMaxWgs16 : kDirectMaxWgs32;
     return (forced || wgs <= max_wgs) ? tiles : 0;
 }

@@ -216,14 +216,10 @@ def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
     need = lib.mha_hd64_plan(1, 4, 1024, 1024, 5242880, out)
     qw, kw, splits, tps = list(out)
     assert need == 0 and (qw, kw, splits) == (22, 4, 1)
-    # 1024 < nkv <= 2048 on 96..256 32-row blocks: the 32-row kernel's two-pass form, no split
+    # 1024 < nkv <= 2048 on <= 256 16-row blocks: the 16-row kernel's two-pass form, no split
     need = lib.mha_hd64_plan(1, 4, 1024, 2048, 5242880, out)
     qw, kw, splits, tps = list(out)
-    assert need == 0 and splits == 1 and qw == 21
-    # on fewer blocks the ring kernel splits the keys within the fixed workspace
-    need = lib.mha_hd64_plan(1, 4, 256, 2048, 5242880, out)
-    qw, kw, splits, tps = list(out)
-    assert need <= 5242880 and splits >= 2 and qw not in (21, 22)
+    assert need == 0 and splits == 1 and qw == 22
     # max length still fits
     need = lib.mha_hd64_plan(1, 4, 2048, 2048, 5242880, out)
     assert need <= 5242880
@@ -241,11 +237,12 @@ def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
     (2, 2048, 1024, 21),     # 512 32-row blocks: two rounds of the 32-row kernel
     (6, 1024, 1024, 21),     # 768: three rounds
     (7, 1024, 1024, None),   # 896 32-row blocks: the LDS ring kernel
-    (1, 1024, 1025, 21),     # more keys than 8 waves x 2 tiles: the 32-row kernel's two passes
-    (1, 2048, 2048, 21),     # two passes on 256 32-row blocks
-    (2, 2048, 2048, None),   # 512 of them: the LDS ring kernel
-    (1, 512, 2048, None),    # 64 of them: the LDS ring kernel's split plan
-    (1, 1024, 2049, None),   # past the plugin's 2048 keys
+    (1, 1024, 1025, 22),     # more keys than 4 waves x 4 tiles: the 16-row kernel's two passes
+    (1, 256, 2048, 22),      # two passes on 64 16-row blocks
+    (1, 2048, 2048, 21),     # 512 16-row blocks: two passes on 256 32-row blocks
+    (1, 2048, 1536, 21),
+    (2, 2048, 2048, None),   # 512 32-row blocks: the LDS ring kernel
+    (1, 1024, 2049, None),   # past 4 waves x 2 x 4 tiles
     (1, 256, 256, 22),
     (1, 1, 1, 22),
     (8, 1024, 1024, None),   # batched: 1024 blocks
@@ -254,8 +251,9 @@ def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
 ])
 def test_planner_single_pass_rule(lib, batch, nq, nkv, code):
     """Single-pass kernels iff fp16 and nkv <= 1024: plan code 22 (16-row blocks) when at most 256
-    of them, else 21 (32-row blocks) when at most 768 of those; 1024 < nkv <= 2048: 21 (two
-    passes) on 96..256 32-row blocks; they need no workspace and never split."""
+    of them, else 21 (32-row blocks) when at most 768 of those; 1024 < nkv <= 2048 (two passes):
+    22 on <= 256 16-row blocks, else 21 on 96..256 32-row blocks; they need no workspace and
+    never split."""
     out = (ctypes.c_int32 * 4)()
     need = lib.mha_hd64_plan(batch, 4, nq, nkv, 5242880, out)
     if code is None:

@@ -496,12 +496,13 @@ def test_direct_kernel_matches_oracle(nq, nkv, code, dev, oracle_mod):
         assert _maxdiff(got[:, :, rows], ref) <= tol
 
 
-# nkv in (1024, 2048]: the 32-row kernel's two-pass form (4 waves x 2 x 4 tiles through 4 slots)
+# nkv in (1024, 2048]: the single-pass kernels' two-pass forms (4 waves x 2 x 4 tiles through 4 slots)
 DIRECT2_SHAPES = [(2048, 2048), (1000, 1500), (64, 2048), (300, 1025), (17, 1900), (1024, 1100), (513, 1537)]
 
 
+@pytest.mark.parametrize("code", [21, 22])
 @pytest.mark.parametrize("nq,nkv", DIRECT2_SHAPES)
-def test_direct_kernel_two_pass_matches_oracle(nq, nkv, dev, oracle_mod):
+def test_direct_kernel_two_pass_matches_oracle(nq, nkv, code, dev, oracle_mod):
     """Second-pass tiles partial or wholly past nkv, waves without keys, both output types."""
     from lightglue_amd import _lib, synth
 
@@ -514,7 +515,7 @@ def test_direct_kernel_two_pass_matches_oracle(nq, nkv, dev, oracle_mod):
     ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
     for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
         o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
-        _forced(lib, q, k, v, o, nq, nkv, 21, 0, 0, ws)
+        _forced(lib, q, k, v, o, nq, nkv, code, 0, 0, ws)
         assert lib.mha_hd64_last_combine_form() == 0
         torch.cuda.synchronize()
         got = o.float().cpu().numpy()
@@ -538,10 +539,11 @@ def test_direct_kernel_two_pass_rescale(dev, oracle_mod):
         ref = oracle_mod.attention_c(q16, k16, v16)
         q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
         for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
-            o = torch.empty(q.shape, dtype=out_dt, device=dev)
-            _forced(lib, q, k, v, o, nq, nkv, 21, 0, 0, ws)
-            torch.cuda.synchronize()
-            assert _maxdiff(o.float().cpu().numpy(), ref) <= tol, (nkv, krow, gain, out_dt)
+            for code in (21, 22):
+                o = torch.empty(q.shape, dtype=out_dt, device=dev)
+                _forced(lib, q, k, v, o, nq, nkv, code, 0, 0, ws)
+                torch.cuda.synchronize()
+                assert _maxdiff(o.float().cpu().numpy(), ref) <= tol, (nkv, krow, gain, out_dt, code)
 
 
 def test_direct_kernel_rescale_and_masked_waves(dev, oracle_mod):
@@ -594,8 +596,7 @@ def test_direct_kernel_forced_outside_its_range_is_rejected(dev):
 
     lib = _lib.load()
     ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
-    for nkv, dt, codes in ((1025, torch.float16, (22,)), (2049, torch.float16, (21, 22)),
-                           (512, torch.float32, (21, 22))):
+    for nkv, dt, codes in ((2049, torch.float16, (21, 22)), (512, torch.float32, (21, 22))):
         q = torch.zeros(1, 4, 64, 64, dtype=dt, device=dev)
         k = torch.zeros(1, 4, nkv, 64, dtype=dt, device=dev)
         o = torch.empty_like(q)
