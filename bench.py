@@ -194,6 +194,31 @@ def load_traffic(tag):
         return None
 
 
+def variants(torch, lightglue_amd, device, stream, q, k, v, flops):
+    """BASELINE configs[2] and the plugin's Float boundary at the metric shape: fp16 in -> fp32 out
+    (the reference's fp16in_fp32out kernel) and fp32 Q/K/V -> fp32 O (a TensorRT fp32 engine's
+    call: convert + fp16 kernel). Per-call time from a graph of 200 back-to-back calls, and the
+    max-abs error against a PyTorch fp32 attention of the same (fp16-valued) inputs on the GPU
+    (lightglue_pytorch_no_plugin/lightglue.py:82-84; north_star tolerance 1e-2)."""
+    qf, kf, vf = (t.float() for t in (q, k, v))
+    ref = torch.softmax((qf @ kf.transpose(-1, -2)) * 0.125, -1) @ vf
+    o32 = torch.empty(q.shape, dtype=torch.float32, device=device)
+    of = torch.empty_like(qf)
+    res = {}
+    for name, fn, o in (("fp16in_fp32out", lambda: lightglue_amd.mha_hd64_batched(q, k, v, out_dtype=torch.float32,
+                                                                                   out=o32), o32),
+                        ("float_boundary", lambda: lightglue_amd.mha_hd64(qf, kf, vf, out=of), of)):
+        o.fill_(float("nan"))
+        with torch.cuda.stream(stream):
+            fn()
+        stream.synchronize()
+        err = float((o - ref).abs().max())
+        t = graph_per_launch_ms(torch, fn, stream)
+        res[name] = {"us_per_call": round(t * 1e3, 3), "calls_per_s": round(1e3 / t, 1),
+                     "tflops": round(flops / (t * 1e-3) / 1e12, 2), "max_abs_vs_torch_fp32": err}
+    return res
+
+
 def concurrent_streams(torch, lightglue_amd, device, nq, nkv, rank, flops, per_stream=500):
     """Independent calls of the metric shape issued on S streams at once (S image pairs in flight,
     each stream its own Q/K/V/O and its own graph of `per_stream` dependent enqueues): whole-GPU
@@ -501,10 +526,11 @@ def main():
         achieved = flops / (t_main * 1e-3) / 1e12
         traffic = load_traffic({22: "direct16_kernel_bytes_per_launch", 21: "direct_kernel_bytes_per_launch"}.get(
             q_waves, "main_kernel_bytes_per_launch"))
-        kname = {22: "mha_hd64_direct16_kernel<f16,4 waves,4 tiles> (single pass: 16 query rows x all 1024 keys "
-                     "per workgroup, no split)",
-                 21: "mha_hd64_direct_kernel<f16,4 waves,4 tiles> (single pass: 32 query rows x all 1024 keys per "
-                     "workgroup, no split)"}.get(
+        two = " in two passes of 4 tiles" if nkv > 1024 else ""
+        kname = {22: f"mha_hd64_direct16_kernel<f16,4 waves,4 tiles> (single pass: 16 query rows x all {nkv} keys "
+                     f"per workgroup{two}, no split)",
+                 21: f"mha_hd64_direct_kernel<f16,4 waves,4 tiles> (single pass: 32 query rows x all {nkv} keys per "
+                     f"workgroup{two}, no split)"}.get(
             q_waves, f"mha_hd64_fwd_kernel<f16,f16,{q_waves},{kv_waves}> ({splits}-way KV split, in-launch combine)")
         result["roofline"] = {
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
@@ -539,6 +565,7 @@ def main():
             "frac": round(B * flops / (tb * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
         }
 
+        result["variants"] = variants(torch, lightglue_amd, device, stream, q, k, v, flops)
         result["concurrent_streams"] = concurrent_streams(torch, lightglue_amd, device, nq, nkv, rank, flops)
         result["matcher_attention"] = matcher_attention(torch, device, stream, rank, separate=args.matcher_separate)
         result["matcher_e2e_fp16"] = matcher_e2e(torch, device, stream, rank)
