@@ -53,12 +53,29 @@ namespace {
 // s_waitcnt vmcnt(N) for a compile-time N (multiples of 8 up to 24)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-    static_assert(N % 8 == 0 && N <= 24, "vmcnt");
+    static_assert(N % 8 == 0 && N <= 40, "vmcnt");
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
 }
+// s_waitcnt vmcnt(8 * groups) for a value known after unrolling
+__device__ __forceinline__ void wait_vm_groups(int groups) {
+    switch (groups) {
+        case 0: wait_vm<0>(); break;
+        case 1: wait_vm<8>(); break;
+        case 2: wait_vm<16>(); break;
+        case 3: wait_vm<24>(); break;
+        case 4: wait_vm<32>(); break;
+        default: wait_vm<40>(); break;
+    }
+}
+
+#ifndef MHA_D2P_EARLY
+#define MHA_D2P_EARLY 1  // two-pass form: second-pass scores between the first pass's PVs (0: after them)
+#endif
 
 // KW waves (key slices) per workgroup x TPW 64-key tiles per wave. (16 waves x 1 tile, four per
 // SIMD, measured 7.7 us against 6.3 us for 8 x 2 at 1x4x1024x1024.)
@@ -236,13 +253,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         // accumulators start from an inline 0. refill: K of tile TPW + t is issued into slot t as
         // soon as V's fragments are in registers (the two-pass form's first pass).
         auto pv = [&](int t, const f16x8(&pt)[2][2], int younger, bool first, bool refill) {
-            switch (younger) {
-                case -1: break;
-                case 0: wait_vm<0>(); break;
-                case 1: wait_vm<8>(); break;
-                case 2: wait_vm<16>(); break;
-                default: wait_vm<24>(); break;
-            }
+            if (younger >= 0) wait_vm_groups(younger);
             if (first) DSTAMP(3);
             const unsigned va0 = region + t * kTileBytes + v_lane + 64 * vb;
             const unsigned va1 = region + t * kTileBytes + v_lane + 64 * (1 - vb);
@@ -395,26 +406,23 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
 #pragma unroll
             for (int t = (TPW > 1 ? 1 : 0); t < TPW; ++t) pv(t, p[t], TPW > 1 ? -1 : 0, TPW == 1, false);
         } else {
-            // First pass's remaining PVs, each refilling its slot with the second pass's K: younger
-            // than V(t) are V(t+1..) and K(TPW..TPW+t-1), always TPW - 1 groups.
-#pragma unroll
-            for (int t = 1; t < TPW; ++t) pv(t, p[t], TPW - 1, false, true);
             // Second pass: tiles TPW + t through slot t, scored against the running max (bias k-step
             // first), ONE rescale decision for the pass (rescaling O and the row sums), exponentials,
             // then PV as each V lands.
             set_bias();
-#pragma unroll
-            for (int t = 0; t < TPW; ++t) {
+            // scores of second-pass tile u (slot u): K(TPW+u) landed (`younger` DMA groups after it),
+            // fragments in registers, V(TPW+u) into the slot, then the MFMAs
+            auto score2 = [&](int u, int younger) {
                 f16x8 kf[8];
-                wait_vm<8 * (TPW - 1)>();  // K(TPW+t) landed: younger are K(TPW+t+1..), V(TPW..TPW+t-1)
-                read_k(t, kf);
+                wait_vm_groups(younger);
+                read_k(u, kf);
                 asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]), "+v"(kf[4]),
                              "+v"(kf[5]), "+v"(kf[6]), "+v"(kf[7])::"memory");
-                dma_tile(v_rs, TPW + t, t);
-                const bool partial = key0 + kTileKV * (TPW + t + 1) > nkv;  // wave-uniform
+                dma_tile(v_rs, TPW + u, u);
+                const bool partial = key0 + kTileKV * (TPW + u + 1) > nkv;  // wave-uniform
                 const f16x8 a_plain = f16x8{one_h, one_h, 0, 0, 0, 0, 0, 0};
-                const f16x8 ab0 = partial ? a_bias_of(TPW + t, 0) : a_plain;
-                const f16x8 ab1 = partial ? a_bias_of(TPW + t, 1) : a_plain;
+                const f16x8 ab0 = partial ? a_bias_of(TPW + u, 0) : a_plain;
+                const f16x8 ab1 = partial ? a_bias_of(TPW + u, 1) : a_plain;
                 f32x16 c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab0, b_bias, f32x16{}, 0, 0, 0);
                 f32x16 c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab1, b_bias, f32x16{}, 0, 0, 0);
 #pragma unroll
@@ -422,8 +430,29 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
                     c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s], qf[s], c0, 0, 0, 0);
                     c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s + 1], qf[s], c1, 0, 0, 0);
                 }
-                sc[t][0] = c0;
-                sc[t][1] = c1;
+                sc[u][0] = c0;
+                sc[u][1] = c1;
+            };
+            // DMA issue order after the first pass's V: K(TPW) at pv(0); then for t = 1..TPW-1 K(TPW+t)
+            // at pv(t) and V(TPW+t-1) at score2(t-1); V(2TPW-1) last.
+            if constexpr (MHA_D2P_EARLY) {
+                // first pass's PVs (each refilling its slot with a second-pass K) interleaved with the
+                // second pass's scores, so each second-pass V is issued one PV after its K
+#pragma unroll
+                for (int t = 1; t < TPW; ++t) {
+                    pv(t, p[t], TPW - 2 + t, false, true);  // V(t): V(t+1..), K(TPW..TPW+t-1), V(TPW..TPW+t-2)
+                    score2(t - 1, t == 1 ? 1 : 2);          // K(TPW+t-1): K(TPW+t) (+ V(TPW+t-2) for t > 1)
+                }
+                DSTAMP(7);
+                score2(TPW - 1, 1);  // K(2TPW-1): V(2TPW-2)
+            } else {
+                // first pass's PVs, each refilling its slot: younger than V(t) are V(t+1..) and
+                // K(TPW..TPW+t-1), always TPW - 1 groups; then the second pass's scores
+#pragma unroll
+                for (int t = 1; t < TPW; ++t) pv(t, p[t], TPW - 1, false, true);
+                DSTAMP(7);
+#pragma unroll
+                for (int t = 0; t < TPW; ++t) score2(t, TPW - 1);  // K(TPW+t): K(TPW+t+1..), V(TPW..TPW+t-1)
             }
             {
                 float mx = -INFINITY;
@@ -446,8 +475,11 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
             }
 #pragma unroll
             for (int t = 0; t < TPW; ++t) exp_pack(sc[t][0], sc[t][1], p[t]);
+            // V(TPW+u) has 2TPW-3-2u younger groups in the interleaved order (none for the last), TPW-1-u
+            // in the sequential one
 #pragma unroll
-            for (int t = 0; t < TPW; ++t) pv(t, p[t], TPW - 1 - t, false, false);
+            for (int t = 0; t < TPW; ++t)
+                pv(t, p[t], MHA_D2P_EARLY ? (t == TPW - 1 ? 0 : 2 * TPW - 3 - 2 * t) : TPW - 1 - t, false, false);
         }
     }
 

@@ -44,4 +44,8 @@ for i, n in enumerate(names):
     d[n + "_med"] = int(statistics.median(seg))
     d[n + "_max"] = int(seg.max())
 d["end_med_from_t0"] = int(statistics.median(t[:, 6] - t0))
+if nkv > 1024 and code == 21:  # two-pass form: slot 7 = second pass starts (first pass's PVs done)
+    d["pass1_start_med_from_t0"] = int(statistics.median(t[:, 7] - t0))
+    d["pass1_med"] = int(statistics.median(t[:, 4] - t[:, 7]))
+    d["v0_to_pass1_med"] = int(statistics.median(t[:, 7] - t[:, 3]))
 print(json.dumps(d))
