@@ -57,11 +57,24 @@ namespace {
 
 template <int N>
 __device__ __forceinline__ void wait_vmc() {
-    static_assert(N % 8 == 0 && N <= 24, "vmcnt");
+    static_assert(N % 8 == 0 && N <= 40, "vmcnt");
     if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+}
+// s_waitcnt vmcnt(8 * groups) for a value known after unrolling
+__device__ __forceinline__ void wait_groups(int groups) {
+    switch (groups) {
+        case 0: wait_vmc<0>(); break;
+        case 1: wait_vmc<8>(); break;
+        case 2: wait_vmc<16>(); break;
+        case 3: wait_vmc<24>(); break;
+        case 4: wait_vmc<32>(); break;
+        default: wait_vmc<40>(); break;
+    }
 }
 
 // max over the lanes of one query (i, i+16, i+32, i+48): v_permlane32_swap then v_permlane16_swap
@@ -329,40 +342,44 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
 #pragma unroll
             for (int t = 1; t < TPW; ++t) pv(t, false, false);
         } else {
-            // pass 0's remaining PVs, each refilling its slot: younger than V(t) are V(t+1..) and
-            // K(TPW..TPW+t-1), always TPW - 1 groups of 8
-#pragma unroll
-            for (int t = 1; t < TPW; ++t) {
-                wait_vmc<8 * (TPW - 1)>();
-                pv(t, false, true);
-            }
-            // pass 1: tiles TPW + t through slot t, raw scores; ONE rescale decision for the pass
-            // (O and the row sums rescaled), then exponentials against the running max and PV
-#pragma unroll
-            for (int t = 0; t < TPW; ++t) {
+            // pass 1: tiles TPW + u through slot u, raw scores; ONE rescale decision for the pass
+            // (O and the row sums rescaled), then exponentials against the running max and PV.
+            // score2(u): K(TPW+u) landed (`younger` DMA groups after it), its fragments in registers,
+            // V(TPW+u) into the slot, the MFMAs.
+            auto score2 = [&](int u, int younger) {
                 f16x8 kf[4][2];
-                wait_vmc<8 * (TPW - 1)>();  // K(TPW+t): younger are K(TPW+t+1..), V(TPW..TPW+t-1)
-                read_k(t, kf);
+                wait_groups(younger);
+                read_k(u, kf);
                 asm volatile("s_waitcnt lgkmcnt(0)"
                              : "+v"(kf[0][0]), "+v"(kf[0][1]), "+v"(kf[1][0]), "+v"(kf[1][1]), "+v"(kf[2][0]),
                                "+v"(kf[2][1]), "+v"(kf[3][0]), "+v"(kf[3][1])::"memory");
-                dma_v(TPW + t, t);
+                dma_v(TPW + u, u);
                 f32x4 c[4];
 #pragma unroll
                 for (int kb = 0; kb < 4; ++kb) {
                     c[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kb][0], qf[0], f32x4{}, 0, 0, 0);
                     c[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kb][1], qf[1], c[kb], 0, 0, 0);
                 }
-                if (key0 + kTileKV * (TPW + t + 1) > nkv) {  // wave-uniform: mask keys past nkv
+                if (key0 + kTileKV * (TPW + u + 1) > nkv) {  // wave-uniform: mask keys past nkv
 #pragma unroll
                     for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
-                            if (key0 + kTileKV * (TPW + t) + 16 * kb + 4 * g + e >= nkv) c[kb][e] = -INFINITY;
+                            if (key0 + kTileKV * (TPW + u) + 16 * kb + 4 * g + e >= nkv) c[kb][e] = -INFINITY;
                 }
 #pragma unroll
-                for (int kb = 0; kb < 4; ++kb) sc[t][kb] = c[kb];
+                for (int kb = 0; kb < 4; ++kb) sc[u][kb] = c[kb];
+            };
+            // pass 0's remaining PVs (each refilling its slot with a pass-1 K) interleaved with
+            // pass 1's scores (mha_hd64_direct.hip's order): DMA issue order after pass 0's V is
+            // K(TPW) at pv(0), then K(TPW+t) at pv(t) and V(TPW+t-1) at score2(t-1), V(2TPW-1) last
+#pragma unroll
+            for (int t = 1; t < TPW; ++t) {
+                wait_groups(TPW - 2 + t);  // V(t): V(t+1..), K(TPW..TPW+t-1), V(TPW..TPW+t-2)
+                pv(t, false, true);
+                score2(t - 1, t == 1 ? 1 : 2);
             }
+            score2(TPW - 1, 1);
             {
                 float mx = -INFINITY;
 #pragma unroll
@@ -381,12 +398,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
             for (int t = 0; t < TPW; ++t) exp_pack(sc[t], p[t], m_run);
 #pragma unroll
             for (int t = 0; t < TPW; ++t) {
-                switch (TPW - 1 - t) {  // V(TPW+t): younger are V(TPW+t+1..)
-                    case 0: wait_vmc<0>(); break;
-                    case 1: wait_vmc<8>(); break;
-                    case 2: wait_vmc<16>(); break;
-                    default: wait_vmc<24>(); break;
-                }
+                wait_groups(t == TPW - 1 ? 0 : 2 * TPW - 3 - 2 * t);  // V(TPW+t): the groups issued after it
                 pv(t, false, false);
             }
         }
