@@ -84,7 +84,8 @@ __device__ __forceinline__ void wait_vm_groups(int groups) {
 // registers, so the second pass's loads queue behind the first pass's without a gap.
 template <typename TOut, int KW, int TPW, bool MULTI, int PASSES = 1>
 __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) {
-    static_assert(PASSES == 1 || (PASSES == 2 && TPW * KW == 16), "two passes: 4 waves x 2 x 4 tiles or 8 x 2 x 2");
+    static_assert(PASSES == 1 || (PASSES == 2 && (TPW * KW == 16 || (TPW == 2 && KW == 4))),
+                  "two passes: 4 waves x 2 x 4 tiles, 8 x 2 x 2, or 4 x 2 x 2 (65 KiB LDS: two workgroups per CU)");
     constexpr int NT = 64 * KW;
     constexpr int BLOCK_M = 32;                         // query rows per workgroup
     constexpr int WAVE_KEYS = kTileKV * TPW * PASSES;   // keys per wave
@@ -558,6 +559,15 @@ hipError_t launch_direct(const FwdArgs& a, int grid, int tiles_per_wave, bool ou
         return !(e && e[0] == '8');
     }();
     // nkv in (1024, 2048] (tiles_per_wave 3, 4): two passes, 4 waves x 2 x 4 tiles (or 8 x 2 x 2)
+    // nkv in (512, 1024] on more than one round of 256 workgroups: 4 waves x two passes of 2 tiles
+    // through 2 slots per wave (65 KiB LDS), so two workgroups share a CU and one's load latency
+    // hides behind the other's work (MHA_HD64_DIRECT_SHARED=0: the one-pass form, one per CU)
+    static const bool shared = [] {
+        const char* e = std::getenv("MHA_HD64_DIRECT_SHARED");
+        return !(e && e[0] == '0');
+    }();
+    if (tiles_per_wave == 2 && grid > 256 && four && shared)
+        return out_f32 ? launch_direct_t<float, 4, 2, 2>(a, grid, stream) : launch_direct_t<f16, 4, 2, 2>(a, grid, stream);
     if (tiles_per_wave > 2) {
         if (four)
             return out_f32 ? launch_direct_t<float, 4, 4, 2>(a, grid, stream)

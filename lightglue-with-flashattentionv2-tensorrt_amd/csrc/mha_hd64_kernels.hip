@@ -983,7 +983,9 @@ static bool direct_enabled() {
 // up to three rounds of 256 still beat the LDS ring's plans there (tools/batch_sweep.py, graph
 // replay, us per launch, 32-row kernel vs planner's ring plan: B=3 N=1024 10.3 vs 18.1, B=6 15.3 vs
 // 19.7, B=6 N=512 6.3 vs 9.5, B=12 N=512 8.7 vs 13.5; at 1024 blocks the ring wins: B=8 N=1024
-// 15.5 vs 21.0, B=16 N=512 10.4 vs 11.2).
+// 15.5 vs 21.0, B=16 N=512 10.4 vs 11.2). Past one round with 512 < nkv <= 1024 the 32-row kernel
+// runs its two-workgroups-per-CU form (launch_direct): B=3 8.86 vs 10.28 for one per CU (ring
+// 10.43), B=4 9.41 vs 10.68 (10.77), B=6 13.15 vs 15.23 (14.11); B=8 16.85 vs ring 15.33.
 constexpr long kDirectMaxWgs16 = 256, kDirectMaxWgs32 = 768;
 static int direct_tiles_for(const Call* calls, int n, InType in, bool forced, int rows = 32) {
     if (in != InType::F16 || (!forced && !direct_enabled())) return 0;

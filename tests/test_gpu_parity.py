@@ -591,6 +591,33 @@ def test_direct_kernel_grouped_and_batched(dev, oracle_mod):
     assert _maxdiff(a.float().cpu().numpy(), oracle_mod.attention_c(*c)) <= TOL
 
 
+def test_direct_kernel_multi_round_shared_form(dev, oracle_mod):
+    """Launches of more than 256 32-row blocks with 512 < nkv <= 1024 run the 4 x 2 x 2-tile two-pass
+    form, two workgroups per CU: batched calls and a grouped layer against the oracle, both output
+    types, sampled rows."""
+    from lightglue_amd import _lib, mha_hd64_batched, mha_hd64_grouped
+
+    lib = _lib.load()
+    for batch, nq, nkv in ((3, 1024, 1024), (2, 2048, 1000), (5, 700, 600)):
+        (c,) = _group_inputs([(batch, nq, nkv)], 17 + batch)
+        q, k, v = (_t(x, dev, torch.float16) for x in c)
+        rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 40)), nq - 1])
+        ref = oracle_mod.attention_c(np.ascontiguousarray(c[0][:, :, rows]), c[1], c[2])
+        for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
+            o = mha_hd64_batched(q, k, v, out_dtype=out_dt)
+            assert lib.mha_hd64_last_combine_form() == 0
+            torch.cuda.synchronize()
+            got = o.float().cpu().numpy()
+            assert np.isfinite(got).all()
+            assert _maxdiff(got[:, :, rows], ref) <= tol, (batch, nq, nkv, out_dt)
+    host = _group_inputs([(1, 2048, 1024), (1, 1024, 2048 - 1100), (1, 1500, 1024)], 29)
+    dev_t = [tuple(_t(x, dev, torch.float16) for x in c) for c in host]
+    outs = mha_hd64_grouped(dev_t)
+    torch.cuda.synchronize()
+    for c, o in zip(host, outs):
+        assert _maxdiff(o.float().cpu().numpy(), oracle_mod.attention_c(*c)) <= TOL
+
+
 def test_direct_kernel_forced_outside_its_range_is_rejected(dev):
     from lightglue_amd import _lib
 
