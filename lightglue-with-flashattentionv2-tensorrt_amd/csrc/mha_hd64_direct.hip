@@ -84,8 +84,9 @@ __device__ __forceinline__ void wait_vm_groups(int groups) {
 // registers, so the second pass's loads queue behind the first pass's without a gap.
 template <typename TOut, int KW, int TPW, bool MULTI, int PASSES = 1>
 __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) {
-    static_assert(PASSES == 1 || (PASSES == 2 && (TPW * KW == 16 || (TPW == 2 && KW == 4))),
-                  "two passes: 4 waves x 2 x 4 tiles, 8 x 2 x 2, or 4 x 2 x 2 (65 KiB LDS: two workgroups per CU)");
+    static_assert(PASSES == 1 || (PASSES == 2 && (TPW * KW == 16 || (TPW == 2 && KW == 4))) ||
+                      (PASSES == 4 && TPW == 2 && KW == 4),
+                  "passes x tiles: 4 waves x 2 x 4, 8 x 2 x 2, or 4 x {2, 4} x 2 (65 KiB LDS: two workgroups per CU)");
     constexpr int NT = 64 * KW;
     constexpr int BLOCK_M = 32;                         // query rows per workgroup
     constexpr int WAVE_KEYS = kTileKV * TPW * PASSES;   // keys per wave
@@ -167,9 +168,9 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
             for (int i = 8 * t0; i < 8 * t1; ++i) dma_piece(k_rs, k_lane[i & 1], i, i);
         };
         // K of tile TPW + t (second pass) into slot t; the swizzle repeats every 2 pieces
-        auto dma_k2 = [&](int t) {
+        auto dma_kt = [&](int tile, int slot) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) dma_piece(k_rs, k_lane[i & 1], 8 * (TPW + t) + i, 8 * t + i);
+            for (int i = 0; i < 8; ++i) dma_piece(k_rs, k_lane[i & 1], 8 * tile + i, 8 * slot + i);
         };
         auto dma_tile = [&](__amdgpu_buffer_rsrc_t rs, int t, int slot) {  // V of tile t into `slot`
 #pragma unroll
@@ -253,7 +254,8 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         // landed: `younger` = DMA groups of 8 issued after it (-1: already waited). first: the
         // accumulators start from an inline 0. refill: K of tile TPW + t is issued into slot t as
         // soon as V's fragments are in registers (the two-pass form's first pass).
-        auto pv = [&](int t, const f16x8(&pt)[2][2], int younger, bool first, bool refill) {
+        auto pv = [&](int t, const f16x8(&pt)[2][2], int younger, bool first, int refill_tile) {
+            const bool refill = refill_tile >= 0;
             if (younger >= 0) wait_vm_groups(younger);
             if (first) DSTAMP(3);
             const unsigned va0 = region + t * kTileBytes + v_lane + 64 * vb;
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
                 asm volatile("s_waitcnt lgkmcnt(0)"
                              : "+v"(vfa[0][0]), "+v"(vfa[0][1]), "+v"(vfa[1][0]), "+v"(vfa[1][1]), "+v"(vfb[0][0]),
                                "+v"(vfb[0][1]), "+v"(vfb[1][0]), "+v"(vfb[1][1])::"memory");
-                dma_k2(t);
+                dma_kt(refill_tile, t);
             }
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj)
@@ -395,7 +397,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
                 m_run += d;
             }
             // tile 0's PV on the matrix pipe beside the later tiles' exponentials (one block)
-            pv(0, p[0], TPW - 1, true, PASSES > 1);
+            pv(0, p[0], TPW - 1, true, PASSES > 1 ? TPW : -1);
 #pragma unroll
             for (int t = 1; t < TPW; ++t) exp_pack(sc[t][0], sc[t][1], p[t]);
         }
@@ -405,25 +407,26 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
             // V has long landed by now: one wait, so the compiler may hoist later fragment reads.
             if constexpr (TPW > 1) wait_vm<0>();
 #pragma unroll
-            for (int t = (TPW > 1 ? 1 : 0); t < TPW; ++t) pv(t, p[t], TPW > 1 ? -1 : 0, TPW == 1, false);
+            for (int t = (TPW > 1 ? 1 : 0); t < TPW; ++t) pv(t, p[t], TPW > 1 ? -1 : 0, TPW == 1, -1);
         } else {
-            // Second pass: tiles TPW + t through slot t, scored against the running max (bias k-step
-            // first), ONE rescale decision for the pass (rescaling O and the row sums), exponentials,
-            // then PV as each V lands.
+            // Later passes: tiles ps·TPW + u through slot u, scored against the running max (bias
+            // k-step first), ONE rescale decision per pass (rescaling O and the row sums),
+            // exponentials, then PV as each V lands, each PV refilling its slot with the next pass's K.
+            constexpr bool EARLY2 = PASSES == 2 && MHA_D2P_EARLY;
             set_bias();
-            // scores of second-pass tile u (slot u): K(TPW+u) landed (`younger` DMA groups after it),
-            // fragments in registers, V(TPW+u) into the slot, then the MFMAs
-            auto score2 = [&](int u, int younger) {
+            // scores of tile `tile` in slot u: its K landed (`younger` DMA groups after it), fragments
+            // in registers, its V into the slot, then the MFMAs
+            auto score2 = [&](int tile, int u, int younger) {
                 f16x8 kf[8];
                 wait_vm_groups(younger);
                 read_k(u, kf);
                 asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kf[0]), "+v"(kf[1]), "+v"(kf[2]), "+v"(kf[3]), "+v"(kf[4]),
                              "+v"(kf[5]), "+v"(kf[6]), "+v"(kf[7])::"memory");
-                dma_tile(v_rs, TPW + u, u);
-                const bool partial = key0 + kTileKV * (TPW + u + 1) > nkv;  // wave-uniform
+                dma_tile(v_rs, tile, u);
+                const bool partial = key0 + kTileKV * (tile + 1) > nkv;  // wave-uniform
                 const f16x8 a_plain = f16x8{one_h, one_h, 0, 0, 0, 0, 0, 0};
-                const f16x8 ab0 = partial ? a_bias_of(TPW + u, 0) : a_plain;
-                const f16x8 ab1 = partial ? a_bias_of(TPW + u, 1) : a_plain;
+                const f16x8 ab0 = partial ? a_bias_of(tile, 0) : a_plain;
+                const f16x8 ab1 = partial ? a_bias_of(tile, 1) : a_plain;
                 f32x16 c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab0, b_bias, f32x16{}, 0, 0, 0);
                 f32x16 c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab1, b_bias, f32x16{}, 0, 0, 0);
 #pragma unroll
@@ -434,53 +437,64 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
                 sc[u][0] = c0;
                 sc[u][1] = c1;
             };
-            // DMA issue order after the first pass's V: K(TPW) at pv(0); then for t = 1..TPW-1 K(TPW+t)
-            // at pv(t) and V(TPW+t-1) at score2(t-1); V(2TPW-1) last.
-            if constexpr (MHA_D2P_EARLY) {
-                // first pass's PVs (each refilling its slot with a second-pass K) interleaved with the
-                // second pass's scores, so each second-pass V is issued one PV after its K
+            if constexpr (EARLY2) {
+                // DMA issue order after the first pass's V: K(TPW) at pv(0); then for t = 1..TPW-1
+                // K(TPW+t) at pv(t) and V(TPW+t-1) at score2(t-1); V(2TPW-1) last. The first pass's
+                // PVs interleave with the second pass's scores, so each second-pass V is issued one
+                // PV after its K.
 #pragma unroll
                 for (int t = 1; t < TPW; ++t) {
-                    pv(t, p[t], TPW - 2 + t, false, true);  // V(t): V(t+1..), K(TPW..TPW+t-1), V(TPW..TPW+t-2)
-                    score2(t - 1, t == 1 ? 1 : 2);          // K(TPW+t-1): K(TPW+t) (+ V(TPW+t-2) for t > 1)
+                    pv(t, p[t], TPW - 2 + t, false, TPW + t);  // V(t): V(t+1..), K(TPW..TPW+t-1), V(TPW..TPW+t-2)
+                    score2(TPW + t - 1, t - 1, t == 1 ? 1 : 2);  // K(TPW+t-1): K(TPW+t) (+ V(TPW+t-2), t > 1)
                 }
                 DSTAMP(7);
-                score2(TPW - 1, 1);  // K(2TPW-1): V(2TPW-2)
+                score2(2 * TPW - 1, TPW - 1, 1);  // K(2TPW-1): V(2TPW-2)
             } else {
-                // first pass's PVs, each refilling its slot: younger than V(t) are V(t+1..) and
-                // K(TPW..TPW+t-1), always TPW - 1 groups; then the second pass's scores
+                // sequential order: every wait has TPW - 1 groups younger than its target (the
+                // pass's later V and the next pass's earlier K, or its later K and earlier V)
 #pragma unroll
-                for (int t = 1; t < TPW; ++t) pv(t, p[t], TPW - 1, false, true);
+                for (int t = 1; t < TPW; ++t) pv(t, p[t], TPW - 1, false, TPW + t);
                 DSTAMP(7);
 #pragma unroll
-                for (int t = 0; t < TPW; ++t) score2(t, TPW - 1);  // K(TPW+t): K(TPW+t+1..), V(TPW..TPW+t-1)
+                for (int u = 0; u < TPW; ++u) score2(TPW + u, u, TPW - 1);
             }
-            {
-                float mx = -INFINITY;
 #pragma unroll
-                for (int t = 0; t < TPW; ++t) mx = fmaxf(mx, tree_max(sc[t][0], sc[t][1]));
-                mx = xhalf_max(mx);
-                if (__builtin_amdgcn_ballot_w64(mx > kRescaleThr) != 0) {
-                    const float d = fmaxf(mx, 0.f);
-                    const float alpha = __builtin_amdgcn_exp2f(-d);
-                    o0 *= alpha;
-                    o1 *= alpha;
-                    l_acc *= alpha;
+            for (int ps = 1; ps < PASSES; ++ps) {
+                if (ps > 1) {
+                    set_bias();
 #pragma unroll
-                    for (int t = 0; t < TPW; ++t) {
-                        sc[t][0] -= d;
-                        sc[t][1] -= d;
-                    }
-                    m_run += d;
+                    for (int u = 0; u < TPW; ++u) score2(ps * TPW + u, u, TPW - 1);
                 }
+                {
+                    float mx = -INFINITY;
+#pragma unroll
+                    for (int t = 0; t < TPW; ++t) mx = fmaxf(mx, tree_max(sc[t][0], sc[t][1]));
+                    mx = xhalf_max(mx);
+                    if (__builtin_amdgcn_ballot_w64(mx > kRescaleThr) != 0) {
+                        const float d = fmaxf(mx, 0.f);
+                        const float alpha = __builtin_amdgcn_exp2f(-d);
+                        o0 *= alpha;
+                        o1 *= alpha;
+                        l_acc *= alpha;
+#pragma unroll
+                        for (int t = 0; t < TPW; ++t) {
+                            sc[t][0] -= d;
+                            sc[t][1] -= d;
+                        }
+                        m_run += d;
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < TPW; ++t) exp_pack(sc[t][0], sc[t][1], p[t]);
+                const bool last = ps == PASSES - 1;
+                // the last pass's V(u) has 2TPW-3-2u younger groups in the interleaved order (none
+                // for the last tile), TPW-1-u in the sequential one; earlier passes refill
+#pragma unroll
+                for (int t = 0; t < TPW; ++t)
+                    pv(t, p[t],
+                       !last ? TPW - 1 : (EARLY2 ? (t == TPW - 1 ? 0 : 2 * TPW - 3 - 2 * t) : TPW - 1 - t), false,
+                       last ? -1 : (ps + 1) * TPW + t);
             }
-#pragma unroll
-            for (int t = 0; t < TPW; ++t) exp_pack(sc[t][0], sc[t][1], p[t]);
-            // V(TPW+u) has 2TPW-3-2u younger groups in the interleaved order (none for the last), TPW-1-u
-            // in the sequential one
-#pragma unroll
-            for (int t = 0; t < TPW; ++t)
-                pv(t, p[t], MHA_D2P_EARLY ? (t == TPW - 1 ? 0 : 2 * TPW - 3 - 2 * t) : TPW - 1 - t, false, false);
         }
     }
 
@@ -568,6 +582,8 @@ hipError_t launch_direct(const FwdArgs& a, int grid, int tiles_per_wave, bool ou
     }();
     if (tiles_per_wave == 2 && grid > 256 && four && shared)
         return out_f32 ? launch_direct_t<float, 4, 2, 2>(a, grid, stream) : launch_direct_t<f16, 4, 2, 2>(a, grid, stream);
+    if (tiles_per_wave > 2 && grid > 256 && four && shared)  // nkv in (1024, 2048], the same: 4 passes of 2
+        return out_f32 ? launch_direct_t<float, 4, 2, 4>(a, grid, stream) : launch_direct_t<f16, 4, 2, 4>(a, grid, stream);
     if (tiles_per_wave > 2) {
         if (four)
             return out_f32 ? launch_direct_t<float, 4, 4, 2>(a, grid, stream)

@@ -998,12 +998,14 @@ static int direct_tiles_for(const Call* calls, int n, InType in, bool forced, in
         tiles = std::max(tiles, (calls[i].nkv + 8 * kTileKV - 1) / (8 * kTileKV));
         wgs += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + rows - 1) / rows);
     }
-    // two-pass forms (tiles 3, 4): one round only — from 512 workgroups on the ring's plans win;
-    // 32-row blocks from 96 on (tools/batch_sweep.py, us per launch, two-pass 16-row / 32-row
+    // two-pass forms (tiles 3, 4), one round: 16-row blocks up to 256, 32-row blocks from 96 on (tools/batch_sweep.py, us per launch, two-pass 16-row / 32-row
     // kernel vs ring plan: 2048^2 B=1 - / 9.87 vs 13.04, B=2 - / 17.6 vs 17.3; 1536^2 B=1 - / 8.13
     // vs 11.12; Nq x Nkv 1024x2048 7.40 / 8.57 vs 10.74, 768x2048 6.79 / 8.38 vs 10.24,
     // 512x2048 6.68 / 8.33 vs 7.95, 256x2048 6.61 / 8.31 vs 7.69, 1024x1536 6.32 / 8.05 vs 9.84)
-    if (tiles > 2 && !forced && (wgs > 256 || (rows == 32 && wgs < 96))) return 0;
+    // Past one round the 32-row kernel's two-workgroups-per-CU form (4 passes x 2 tiles) takes
+    // over up to 768 blocks (vs the ring plan: 2x4x2048^2 16.1 vs 17.8, 3x 21.7 vs 23.3; 2x4x1536^2
+    // 12.0 vs 13.5, 3x 18.0 vs 17.7, 4x 18.6 vs 18.7; 4x4x1024x2048 15.0 vs 17.8).
+    if (tiles > 2 && !forced && (rows == 16 ? wgs > 256 : wgs < 96)) return 0;
     const long max_wgs = rows == 16 ? kDirectMaxWgs16 : kDirectMaxWgs32;
     return (forced || wgs <= max_wgs) ? tiles : 0;
 }

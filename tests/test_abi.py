@@ -241,7 +241,8 @@ def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
     (1, 256, 2048, 22),      # two passes on 64 16-row blocks
     (1, 2048, 2048, 21),     # 512 16-row blocks: two passes on 256 32-row blocks
     (1, 2048, 1536, 21),
-    (2, 2048, 2048, None),   # 512 32-row blocks: the LDS ring kernel
+    (2, 2048, 2048, 21),     # 512 32-row blocks: 4 passes x 2 tiles, two workgroups per CU
+    (4, 2048, 2048, None),   # 1024 of them: the LDS ring kernel
     (1, 1024, 2049, None),   # past 4 waves x 2 x 4 tiles
     (1, 256, 256, 22),
     (1, 1, 1, 22),
@@ -252,7 +253,7 @@ def test_plan_fills_the_chip_and_fits_the_reference_workspace(lib):
 def test_planner_single_pass_rule(lib, batch, nq, nkv, code):
     """Single-pass kernels iff fp16 and nkv <= 1024: plan code 22 (16-row blocks) when at most 256
     of them, else 21 (32-row blocks) when at most 768 of those; 1024 < nkv <= 2048 (two passes):
-    22 on <= 256 16-row blocks, else 21 on 96..256 32-row blocks; they need no workspace and
+    22 on <= 256 16-row blocks, else 21 on 96..768 32-row blocks; they need no workspace and
     never split."""
     out = (ctypes.c_int32 * 4)()
     need = lib.mha_hd64_plan(batch, 4, nq, nkv, 5242880, out)

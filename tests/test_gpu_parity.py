@@ -610,6 +610,23 @@ def test_direct_kernel_multi_round_shared_form(dev, oracle_mod):
             got = o.float().cpu().numpy()
             assert np.isfinite(got).all()
             assert _maxdiff(got[:, :, rows], ref) <= tol, (batch, nq, nkv, out_dt)
+    # 1024 < nkv <= 2048 past one round (forced plan 21): the 4 x 4 passes x 2-tile form
+    for batch, nq, nkv in ((2, 2048, 2048), (3, 1100, 1300)):
+        (c,) = _group_inputs([(batch, nq, nkv)], 23 + batch)
+        q, k, v = (_t(x, dev, torch.float16) for x in c)
+        rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 40)), nq - 1])
+        ref = oracle_mod.attention_c(np.ascontiguousarray(c[0][:, :, rows]), c[1], c[2])
+        ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+        for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
+            o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
+            st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), batch, 4, nq, nkv,
+                                            0, int(out_dt == torch.float32), 21, 0, 0, ws.data_ptr(), ws.numel(),
+                                            torch.cuda.current_stream().cuda_stream, 3)
+            assert st == 0, _lib.last_error()
+            torch.cuda.synchronize()
+            got = o.float().cpu().numpy()
+            assert np.isfinite(got).all()
+            assert _maxdiff(got[:, :, rows], ref) <= tol, (batch, nq, nkv, out_dt)
     host = _group_inputs([(1, 2048, 1024), (1, 1024, 2048 - 1100), (1, 1500, 1024)], 29)
     dev_t = [tuple(_t(x, dev, torch.float16) for x in c) for c in host]
     outs = mha_hd64_grouped(dev_t)
