@@ -546,6 +546,31 @@ def test_direct_kernel_two_pass_rescale(dev, oracle_mod):
                 assert _maxdiff(o.float().cpu().numpy(), ref) <= tol, (nkv, krow, gain, out_dt, code)
 
 
+def test_direct_kernel_four_pass_rescale(dev, oracle_mod):
+    """The two-per-CU 4-pass form (forced plan 21, B = 2 so the launch has > 256 blocks): spikes in
+    the third and fourth passes of a wave move the running max late (key 300: wave 0, pass 2; key
+    480: wave 0, pass 3; key 1900: wave 3, pass 2), and nkv = 1100 leaves waves 2-3 short."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    nq, batch = 1024, 2
+    for nkv, krow, gain in ((2048, 300, 6.0), (2048, 480, 3.0), (2048, 1900, 6.0), (1100, 1090, 6.0)):
+        qn, kn, vn = synth.qkv(808 + nkv + krow, nq, nkv, batch=batch)
+        kn = synth.spike(qn, kn, 5, krow, gain)
+        q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
+        rows = np.unique(np.r_[np.arange(0, nq, 37), 5, nq - 1])
+        ref = oracle_mod.attention_c(np.ascontiguousarray(q16[:, :, rows]), k16, v16)
+        q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+        o = torch.full(q.shape, float("nan"), dtype=torch.float16, device=dev)
+        st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), batch, 4, nq, nkv, 0,
+                                        0, 21, 0, 0, ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream,
+                                        3)
+        assert st == 0, _lib.last_error()
+        torch.cuda.synchronize()
+        assert _maxdiff(o.float().cpu().numpy()[:, :, rows], ref) <= TOL, (nkv, krow, gain)
+
+
 def test_direct_kernel_rescale_and_masked_waves(dev, oracle_mod):
     """A spike in a wave's second tile forces the rescale of the first tile's probabilities (key
     100: wave 0, tile 1; key 1000: wave 7, tile 1); nkv = 600 leaves waves 5-7 without keys."""
