@@ -2,7 +2,7 @@
 
 Run in the build container only (it reads /root/reference, which is absent on the GPU box):
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [case ...]   # all cases, or only the named ones
 
 It loads the reference's oracle module file directly
 (/root/reference/lightglue_pytorch_no_plugin/lightglue.py; importing the package fails
@@ -48,6 +48,8 @@ CASES = {
     "spike128x300": (19, 128, 300, 1.0, 1.0, (5, 250, 4.0), True),
     "t1024": (20, 1024, 1024, 1.0, 1.0, None, False),      # BASELINE configs[1] shape
     "t33x65": (21, 33, 65, 1.0, 1.0, None, True),
+    "t2048": (22, 2048, 2048, 1.0, 1.0, None, False),      # plugin maximum: the two-pass kernel
+    "cross1536x1300": (23, 1536, 1300, 1.0, 1.0, None, False),
 }
 ROW_STRIDE = 16  # rows kept for non-full cases: 0, 16, 32, ... and the last row
 
@@ -71,8 +73,15 @@ def main() -> None:
     ref_np = load_module(os.path.join(REF, "lightglue_pytorch_no_plugin", "lightglue.py"), "ref_lg_no_plugin")
     ref_wp = load_module(os.path.join(REF, "lightglue_pytorch_with_plugin", "lightglue.py"), "ref_lg_with_plugin")
     attn = ref_np.Attention()
+    only = set(sys.argv[1:])
     index = {}
+    index_path = os.path.join(HERE, "index.json")
+    if only and os.path.exists(index_path):
+        with open(index_path) as f:
+            index = json.load(f)["cases"]
     for name, (seed, nq, nkv, q_std, kv_std, spk, full) in CASES.items():
+        if only and name not in only:
+            continue
         q, k, v = make_inputs(seed, nq, nkv, q_std, kv_std, spk)
         q16, k16, v16 = synth.round_f16(q), synth.round_f16(k), synth.round_f16(v)
         with torch.no_grad():
@@ -102,7 +111,7 @@ def main() -> None:
                            rows=int(rows.size), sdpa_maxdev=sdpa_dev, bytes=os.path.getsize(path))
         print(f"{name:16s} nq={nq:5d} nkv={nkv:5d} rows={rows.size:5d} sdpa_dev={sdpa_dev:.2e} "
               f"{os.path.getsize(path)/1024:.0f} KiB")
-    with open(os.path.join(HERE, "index.json"), "w") as f:
+    with open(index_path, "w") as f:
         json.dump(dict(generator="tests/golden/make_golden.py",
                        reference="lightglue_pytorch_no_plugin/lightglue.py:75-85 (Attention.forward)",
                        cross_check="lightglue_pytorch_with_plugin/lightglue.py:16-46 (MHAHeadDim64.apply, SDPA)",
