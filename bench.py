@@ -472,6 +472,9 @@ def main():
         "vs_baseline": None,
         "dtype": "fp16",
         "data": "synthetic",
+        # an image pair is 36 such calls (9 layers x 2 self + 2 cross), so the
+        # attention-only pair rate of the whole job is value / 36 (matcher_e2e_fp16 times whole pairs)
+        "attention_pairs_per_s": round(value / 36, 1),
         "config": {"workload": "MHAHeadDim64 plugin enqueue, Q/K/V [1,4,1024,64] fp16 -> O fp16 "
                                "(BASELINE configs[1]); K independent calls per step-graph",
                    "batch": 1, "heads": 4, "nq": nq, "nkv": nkv, "head_dim": 64,
