@@ -698,6 +698,32 @@ def test_direct_kernel_deterministic_and_capturable(dev):
     assert torch.equal(a, b) and torch.equal(out, a)
 
 
+@pytest.mark.parametrize("nq,nkv", [(1, 2048), (2048, 1), (2048, 1025), (1025, 2048), (17, 1537), (1536, 1536),
+                                     (2047, 2047), (1024, 1088)])
+def test_planner_default_edges(nq, nkv, dev, oracle_mod):
+    """Edges of the planner's single-pass ranges (1024 / 2048 keys, 256 / 768 blocks) through the
+    default plan, both output types, against the C oracle on sampled rows."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    qn, kn, vn = synth.qkv(4242 + nq + 7 * nkv, nq, nkv)
+    q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
+    rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 24)), nq - 1])
+    ref = oracle_mod.attention_c(np.ascontiguousarray(q16[:, :, rows]), k16, v16)
+    q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+    ws = torch.empty(5242880, dtype=torch.uint8, device=dev)
+    for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
+        o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
+        st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), 1, 4, nq, nkv, 0,
+                                        int(out_dt == torch.float32), 0, 0, 0, ws.data_ptr(), ws.numel(),
+                                        torch.cuda.current_stream().cuda_stream, 3)
+        assert st == 0, _lib.last_error()
+        torch.cuda.synchronize()
+        got = o.float().cpu().numpy()
+        assert np.isfinite(got).all(), (nq, nkv)
+        assert _maxdiff(got[:, :, rows], ref) <= tol, (nq, nkv, out_dt)
+
+
 def test_planner_default_random_shapes(dev, oracle_mod):
     """Seeded random shapes through the planner's default plan (single-pass kernel or LDS ring,
     split or not) for both output types, against the C oracle on sampled rows."""
