@@ -418,8 +418,13 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
     }
     __syncthreads();
     DSTAMP(5);
-    if (KW > 4 && tid >= 256) return;  // 256 threads merge (row, 4 dims)
-    const int row = tid >> 4, c = (tid & 15) * 4;
+#ifndef MHA_D16_EPI8
+#define MHA_D16_EPI8 0  // 1: 128 threads merge (row, 8 dims) with 16-B stores (A/B hook)
+#endif
+    constexpr int EDPT = MHA_D16_EPI8 ? 8 : 4;            // dims per merging thread
+    constexpr int EMERGE = BLOCK_M * kHeadDim / EDPT;     // merging threads
+    if (EMERGE < 64 * KW && tid >= EMERGE) return;
+    const int row = tid / (kHeadDim / EDPT), c = (tid % (kHeadDim / EDPT)) * EDPT;
     const int q = qtile * BLOCK_M + row;
     float2 ml[KW];
     float M = -INFINITY;
@@ -428,19 +433,22 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         ml[k] = *reinterpret_cast<const float2*>(mlb + (k * BLOCK_M + row) * 2);
         M = fmaxf(M, ml[k].x);
     }
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     float L = 0.f;
 #pragma unroll
     for (int k = 0; k < KW; ++k) {
         const float w = (ml[k].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[k].x - M);
         L += w * ml[k].y;
-        acc += w * *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(smem + k * RS) + row * OROW + c);
+        const float* src = reinterpret_cast<const float*>(smem + k * RS) + row * OROW + c;
+        acc += w * *reinterpret_cast<const f32x4*>(src);
+        if constexpr (EDPT == 8) acc1 += w * *reinterpret_cast<const f32x4*>(src + 4);
     }
     if (q < nq) {
         const __amdgpu_buffer_rsrc_t o_rs = make_rsrc(reinterpret_cast<TOut*>(ca.o) + (size_t)bh * nq * kHeadDim,
                                                       (unsigned)(nq * kHeadDim * sizeof(TOut)));
         const float inv = 1.f / L;
-        store_dims<TOut, 4, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)), acc * inv, acc * inv);
+        store_dims<TOut, EDPT, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)), acc * inv,
+                                           acc1 * inv);
     }
 #ifdef MHA_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
