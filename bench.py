@@ -527,6 +527,7 @@ def main():
         lib.mha_hd64_set_fused_combine(1)
         t_call = statistics.median(event_durations_ms(torch, full_call, 200, stream)[20:])
         achieved = flops / (t_main * 1e-3) / 1e12
+        mfma_busy = load_traffic("direct16_mfma_busy_cycles_per_simd")
         traffic = load_traffic({22: "direct16_kernel_bytes_per_launch", 21: "direct_kernel_bytes_per_launch"}.get(
             q_waves, "main_kernel_bytes_per_launch"))
         two = " in two passes of 4 tiles" if nkv > 1024 else ""
@@ -538,6 +539,12 @@ def main():
         result["roofline"] = {
             "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": traffic,
+            # from the committed PMC passes (profiles/traffic.json): measured HBM bytes per launch over
+            # this run's kernel time, and SQ_VALU_MFMA_BUSY_CYCLES per SIMD over the kernel's cycles
+            # at the 2.4 GHz peak clock (a lower bound on the busy fraction at the clock held)
+            "hbm_gbs_measured_bytes": None if traffic is None else round(traffic / (t_main * 1e-3) / 1e9, 1),
+            "mfma_busy_frac_pmc": (None if mfma_busy is None or q_waves != 22
+                                   else round(mfma_busy / (t_main * 1e-3 * 2.4e9), 4)),
             "kernel": kname,
             "kernel_us": round(t_main * 1e3, 3),
             "direct32_kernel_us": None if t_direct32 is None else round(t_direct32 * 1e3, 3),
