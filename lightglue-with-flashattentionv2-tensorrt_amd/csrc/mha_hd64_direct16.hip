@@ -206,12 +206,19 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         // Q (B operand of Sᵀ = K·Qᵀ): Q[q_row][32s+8g..+7], by inline-asm loads (outside the
         // compiler's wait bookkeeping, which would drain every DMA at their use)
         f16x8 qraw[2], qf[2];
+#ifndef MHA_D16_K0_FIRST
+#define MHA_D16_K0_FIRST 0  // 1: K(0)'s DMA ahead of the Q loads for every form (A/B hook)
+#endif
+        // K(0)'s DMA ahead of the Q loads (same wait counts) for the 2-tile form: 1x4x512^2 3.36-3.40
+        // vs 3.42-3.52 us; the 4-tile form (the metric call) keeps Q first (4.97-5.04 vs 4.89-4.99)
+        constexpr bool K0F = MHA_D16_K0_FIRST || (TPW == 2 && PASSES == 1);
+        if constexpr (K0F) dma_k(0, 1);
 #pragma unroll
         for (int s = 0; s < 2; ++s)
             asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen"
                          : "=v"(qraw[s])
                          : "v"((unsigned)(q_row * kHeadDim + 32 * s + 8 * g) * 2), "s"(q_rs));
-        dma_k(0, 2);
+        dma_k(K0F ? 1 : 0, 2);
         wait_vmc<8>();  // Q and K(0) landed (younger: K(1))
         asm volatile("" : "+v"(qraw[0]), "+v"(qraw[1])::"memory");
         DSTAMP(1);
