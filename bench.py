@@ -57,6 +57,47 @@ def dist_env():
     return ws, rank, local
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_devices():
+    """GPU count without initialising the HIP runtime in this process (torch.cuda.device_count()
+    does not, on this image), so the launcher may still start its ranks afterwards."""
+    import torch
+
+    return torch.cuda.device_count()
+
+
+def launch_replicas(n, argv, count_devices=visible_devices, python=sys.executable, script=None):
+    """`bench.py --gpus N` without a torchrun environment: start N rank processes (RANK,
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT set; rank r drives device r) before anything touches
+    the GPU, wait for all of them and return the first non-zero exit status (0 if all passed).
+    Fewer than N visible devices is an error, not a silent N=1 run (one pair
+    stream per GPU, the reference's pair loop demo/demo_mono.cpp:194-418 replicated)."""
+    import subprocess
+
+    have = count_devices()
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}", file=sys.stderr, flush=True)
+        return 2
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([python, script or os.path.abspath(__file__)] + list(argv), env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
 def timed_region(run_steps, barrier, sync, reduce_max):
     """barrier + sync, run the K steps, sync + barrier; return max-over-ranks seconds."""
     barrier()
@@ -69,7 +110,56 @@ def timed_region(run_steps, barrier, sync, reduce_max):
     return reduce_max(dt)
 
 
-def make_collectives(torch, dist, device):
+def timed_replays(torch, replay, stream, barrier, reduce_max, replays):
+    """The headline's timed region: barrier + synchronize, then `replays` replays of the K-step
+    graph back to back on the launch stream with a HIP event pair around each (events on the stream
+    the kernels run on), synchronize + barrier. Returns (max over ranks of the median replay time,
+    max over ranks of the host wall time per replay), in seconds.
+
+    The event pair times exactly the K steps on the GPU. A sleep kernel queued ahead of the replays
+    holds the stream while the host submits them (sized from an untimed rehearsal of the host's
+    submission time), so the GPU runs them back to back: the host's graph-launch cost at a short K
+    (~0.1 ms per 20-node replay here, about the GPU time of the 20 calls) stays out of the events
+    instead of starving the GPU between calls."""
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(replays)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(replays)]
+
+    def submit():
+        t = time.perf_counter()
+        with torch.cuda.stream(stream):
+            for i in range(replays):
+                starts[i].record(stream)
+                replay()
+                ends[i].record(stream)
+        return time.perf_counter() - t
+
+    # untimed rehearsal: host submission time, and the sleep kernel's rate on this device
+    host_s = submit()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        e0.record(stream)
+        torch.cuda._sleep(int(1e7))
+        e1.record(stream)
+    torch.cuda.synchronize()
+    cycles_per_s = 1e7 / max(1e-6, e0.elapsed_time(e1) * 1e-3)
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(int(cycles_per_s * (1.5 * host_s + 2e-3)))
+    submit()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / replays
+    barrier()
+    med = statistics.median(s.elapsed_time(e) for s, e in zip(starts, ends)) * 1e-3
+    return reduce_max(med), reduce_max(wall)
+
+
+def make_collectives(torch, dist, device=None):
+    """Barrier and max-reduce over ranks on a CPU (gloo) group: the replicas exchange nothing on
+    the data path, so no RCCL communicator is created (north_star: no collectives needed)."""
     if dist is None or not dist.is_initialized():
         return (lambda: None), (lambda x: x)
 
@@ -77,11 +167,44 @@ def make_collectives(torch, dist, device):
         dist.barrier()
 
     def reduce_max(x):
-        t = torch.tensor([x], dtype=torch.float64, device=device)
+        t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     return barrier, reduce_max
+
+
+def gather(dist, obj):
+    """Every rank's `obj`, in rank order (a list of one when single-process)."""
+    if dist is None or not dist.is_initialized():
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def cpu_share():
+    """CPUs this process may use: the affinity mask, capped by a cgroup v2 CPU quota and by
+    OMP_NUM_THREADS when the environment sets it (a gpurun box reports the whole host's CPUs in
+    os.cpu_count() and in the affinity mask but grants this job a share of them, stated there as
+    OMP_NUM_THREADS=16). Returns (threads to use, affinity count, cgroup quota or None)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    use = min(n, quota) if quota else n
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:  # the box's stated CPU share for this job
+        use = min(use, int(omp))
+    return use, n, quota
 
 
 # ----------------------------------------------------------------------------------------
@@ -142,14 +265,17 @@ def graph_per_launch_ms(torch, launch, stream, k=200, reps=5):
 def cpu_baseline(seconds=10.0, nq=1024, nkv=1024):
     """Reference PyTorch CPU attention (lightglue_pytorch_no_plugin/lightglue.py:82-84, restated
     in oracle/oracle.py) on this host, fp32, bounded sample of ~`seconds` at the metric shape
-    with all torch threads; plus the SURVEY §8(d) grid (1 thread / all threads x 256^2 / 1024^2,
-    20 warm-ups then the median of >= 50 calls)."""
+    with every CPU this process is granted (cpu_share(): affinity mask capped by the cgroup quota;
+    SURVEY §8(d) asks for os.cpu_count(), which on a shared GPU box counts the whole host); plus
+    the SURVEY §8(d) grid (1 thread / all granted threads x 256^2 / 1024^2, 20 warm-ups then the
+    median of >= 50 calls)."""
     import torch
 
     from lightglue_amd import synth
     from oracle import oracle
 
-    threads = torch.get_num_threads()
+    threads, affinity, quota = cpu_share()
+    torch.set_num_threads(threads)
 
     def median_ms(n_q, n_kv, nthreads, min_calls, budget_s):
         torch.set_num_threads(nthreads)
@@ -178,7 +304,12 @@ def cpu_baseline(seconds=10.0, nq=1024, nkv=1024):
             "ms_per_call": round(med, 3),
             "sample": f"{n} calls of 1x4x{nq}x{nkv} d=64 fp32, torch CPU matmul-softmax-matmul "
                       f"(reference Attention.forward math), median per call, {threads} threads, ~{seconds:.0f}s",
-            "grid": grid, "cpu_model": _cpu_model(), "host_logical_cpus": os.cpu_count()}
+            "grid": grid, "cpu_model": _cpu_model(), "host_logical_cpus": os.cpu_count(),
+            "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "threads_note": (f"{threads} threads = the CPUs granted to this process (affinity {affinity}, "
+                             f"cgroup quota {quota}, OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS')}); "
+                             f"os.cpu_count() = {os.cpu_count()} counts the whole host, which other jobs share"),
+            "single_thread_ms_per_call": grid.get(f"{nq}x{nkv}_1T_ms")}
 
 
 def load_traffic(tag):
@@ -407,19 +538,31 @@ def main():
     ap.add_argument("--sweep", action="store_true", help="time every workgroup shape x KV split (stderr table)")
     ap.add_argument("--only", choices=["call", "batched"], default=None,
                     help="profiling driver: launch just this workload --steps times (eager), print nothing else")
+    ap.add_argument("--replays", type=int, default=0,
+                    help="replays of the K-step graph in the timed region (median taken; 0: enough for ~20k calls)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU, started before anything touches the GPU (no exec from this process)
+        sys.exit(launch_replicas(args.gpus, sys.argv[1:]))
 
     import torch
 
     ws, rank, local = dist_env()
+    if ws != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if visible_devices() <= local:
+        print(f"bench.py: rank {rank} needs GPU {local}, {visible_devices()} visible", file=sys.stderr, flush=True)
+        sys.exit(2)
     dist = None
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     if ws > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=device)
-    barrier, reduce_max = make_collectives(torch, dist, device)
+        dist.init_process_group("gloo")  # CPU barrier / timer reduce only; no RCCL on the data path
+    barrier, reduce_max = make_collectives(torch, dist)
 
     import lightglue_amd
     from lightglue_amd import _lib, synth
@@ -448,10 +591,36 @@ def main():
     graph.replay()                                   # upload / first-replay cost outside the timer
     stream.synchronize()
 
-    elapsed = timed_region(lambda: graph.replay(), barrier, lambda: torch.cuda.synchronize(device), reduce_max)
+    replays = args.replays if args.replays > 0 else max(10, min(250, -(-5000 // args.steps)))
+    elapsed, wall = timed_replays(torch, graph.replay, stream, barrier, reduce_max, replays)
     total_calls = args.steps * ws
     value = total_calls / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
+    rank_values = gather(dist, round(args.steps / elapsed, 1))
+    # Each replay of a K-step graph pays a fixed ~9 us of graph launch + ~4.8 us for its event pair
+    # on the GPU (tools/timing_probe.py, profiles/r02/timing_probe.txt); at the driver's K = 20
+    # that is ~10 % of the step time. The same calls in 2000-step graphs, for comparison:
+    long_rate = None
+    if args.steps < 2000:
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2, stream=stream):
+            for _ in range(2000):
+                lightglue_amd.mha_hd64(q, k, v, out=out)
+        g2.replay()
+        stream.synchronize()
+        t_long, _ = timed_replays(torch, g2.replay, stream, barrier, reduce_max, 5)
+        long_rate = round(2000 * ws / t_long, 1)
+        del g2
+
+    # Bit-identity across devices: every rank runs the same seeded pair-call and hashes its output.
+    import hashlib
+
+    cq, ck, cv = (torch.from_numpy(x).to(device).half().contiguous() for x in synth.qkv(4242, nq, nkv))
+    co = torch.empty_like(cq)
+    with torch.cuda.stream(stream):
+        lightglue_amd.mha_hd64(cq, ck, cv, out=co)
+    stream.synchronize()
+    digests = gather(dist, hashlib.sha256(co.cpu().numpy().tobytes()).hexdigest()[:16])
 
     import ctypes
 
@@ -475,10 +644,18 @@ def main():
         # an image pair is 36 such calls (9 layers x 2 self + 2 cross), so the
         # attention-only pair rate of the whole job is value / 36 (matcher_e2e_fp16 times whole pairs)
         "attention_pairs_per_s": round(value / 36, 1),
+        "timing": {"replays": replays, "per_replay": "HIP events on the launch stream around one replay of the "
+                                                     "K-step graph; median over replays, max over ranks; replays "
+                                                     "queued behind a sleep kernel so host submission does not gap "
+                                                     "the GPU",
+                   "host_wall_ms_per_replay": round(wall * 1e3, 4),
+                   "calls_per_s_in_2000_step_graphs": long_rate},
+        "per_rank_calls_per_s": rank_values,
+        "outputs_bitwise_identical_across_ranks": len(set(digests)) == 1,
         "config": {"workload": "MHAHeadDim64 plugin enqueue, Q/K/V [1,4,1024,64] fp16 -> O fp16 "
                                "(BASELINE configs[1]); K independent calls per step-graph",
                    "batch": 1, "heads": 4, "nq": nq, "nkv": nkv, "head_dim": 64,
-                   "parallelism": f"replicas{ws}",
+                   "parallelism": f"replicas{ws}", "pairs": "one pair stream per GPU, no collective",
                    "plan": {"q_waves": q_waves, "kv_waves": kv_waves, "kv_splits": splits}},
     }
 
@@ -579,10 +756,25 @@ def main():
             "frac": round(B * flops / (tb * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
         }
 
+        # The 70 % bar read against the saturated form: one call alone is bounded by the dependent
+        # launch boundary (MI355X_MICROARCH.md price list, row 'boundary': 1.45 us between trivial
+        # 256-workgroup kernels) against an ideal 0.43 us of MFMA work.
+        result["roofline"]["ideal_us_at_peak"] = round(flops / (PEAK_F16_TFLOPS * 1e12) * 1e6, 4)
+        result["roofline"]["launch_boundary_floor_us"] = 1.45
+        result["roofline"]["saturated"] = {"form": f"{B} calls per launch (batched)",
+                                           "frac": result["batched"]["frac"],
+                                           "tflops": result["batched"]["tflops"]}
+
         result["variants"] = variants(torch, lightglue_amd, device, stream, q, k, v, flops)
         result["concurrent_streams"] = concurrent_streams(torch, lightglue_amd, device, nq, nkv, rank, flops)
         result["matcher_attention"] = matcher_attention(torch, device, stream, rank, separate=args.matcher_separate)
         result["matcher_e2e_fp16"] = matcher_e2e(torch, device, stream, rank)
+        # whole-job pair rate (BASELINE configs[4]): each GPU streams its own pairs through the matcher
+        pair_rates = gather(dist, result["matcher_e2e_fp16"][str(nq)]["pairs_per_s"]
+                            if str(nq) in result["matcher_e2e_fp16"] else None)
+        if all(p is not None for p in pair_rates):
+            result["pairs_per_s_all_gpus"] = {"matcher_e2e_fp16": round(sum(pair_rates), 1), "n": nq,
+                                              "per_rank": pair_rates}
 
     if args.sweep and rank == 0:
         sweep(torch, lib, device, stream, nq, nkv)

@@ -893,7 +893,8 @@ void set_stamp_buffer(void* p) { g_stamps = reinterpret_cast<unsigned long long*
 //    stream may be replayed side by side).
 // Arrays are created only outside capture (hipMalloc + memset, then a one-time stream sync for the
 // arena); a launch that finds no tickets combines in the second kernel instead. Nothing is freed
-// (a launch in flight or a graph may still reference it).
+// (a launch in flight or a graph may still reference it); a half-used arena is replaced at the
+// next eager launch (tickets_for).
 namespace {
 int g_fused = -1;  // -1: unset (env MHA_HD64_FUSED_COMBINE, default on), 0 off, 1 on
 std::mutex g_ticket_mu;
@@ -948,10 +949,19 @@ static unsigned* tickets_for(hipStream_t stream, int count) {
         ar.used += n;
         return p;
     }
-    if (!ar.base) {  // first eager launch on this device: the arena for later captures
-        ar.base = zeroed_tickets(kArenaTickets, stream);
-        if (ar.base && hipStreamSynchronize(stream) == hipSuccess) ar.cap = kArenaTickets;
-        else ar.base = nullptr;
+    // First eager launch on this device: the arena for later captures. An arena more than half
+    // carved is replaced by a fresh one at the next eager launch (the old one stays allocated: graphs
+    // recorded from it may still run), so captures run out only after 512 Ki tickets recorded with
+    // no eager launch in between.
+    if (!ar.base || ar.used > ar.cap / 2) {
+        unsigned* fresh = zeroed_tickets(kArenaTickets, stream);
+        if (fresh && hipStreamSynchronize(stream) == hipSuccess) {
+            ar.base = fresh;
+            ar.cap = kArenaTickets;
+            ar.used = 0;
+        } else if (!ar.base) {
+            ar.cap = 0;
+        }
     }
     auto& slot = g_tickets[{dev, stream}];
     if (slot.first && slot.second >= count) return slot.first;

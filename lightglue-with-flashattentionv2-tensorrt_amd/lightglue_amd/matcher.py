@@ -475,12 +475,21 @@ def seeded_state_dict(seed: int, n_layers: int = 9, descriptor_dim: int = 256, i
     return out
 
 
-def synthetic_pair(seed: int, m: int, n: int, input_dim: int = 256):
-    """Keypoints in the normalised [-1, 1] frame and unit-norm descriptors, fp32, batch 1."""
+def synthetic_pair(seed: int, m: int, n: int, input_dim: int = 256, overlap: int = 0):
+    """Keypoints in the normalised [-1, 1] frame and unit-norm descriptors, fp32, batch 1.
+
+    overlap > 0: the first `overlap` keypoints of image 1 re-observe distinct keypoints of image 0
+    (a seeded permutation; positions moved by ~0.01, descriptors perturbed by 0.2-std noise and
+    renormalised), so the pair has real correspondences for the matcher to find."""
     k0 = synth.uniform24(seed * 4 + 0, m * 2).reshape(1, m, 2) * 2.0 - 1.0
     k1 = synth.uniform24(seed * 4 + 1, n * 2).reshape(1, n, 2) * 2.0 - 1.0
     d0 = synth.normal(seed * 4 + 2, (1, m, input_dim))
     d1 = synth.normal(seed * 4 + 3, (1, n, input_dim))
     d0 = d0 / np.linalg.norm(d0, axis=-1, keepdims=True)
+    if overlap > 0:
+        assert overlap <= min(m, n)
+        src = np.argsort(synth.uniform24(seed * 4 + 5, m), kind="stable")[:overlap]
+        k1[0, :overlap] = k0[0, src] + 0.01 * synth.normal(seed * 4 + 6, (overlap, 2))
+        d1[0, :overlap] = d0[0, src] + 0.2 * synth.normal(seed * 4 + 7, (overlap, input_dim)) / np.sqrt(input_dim)
     d1 = d1 / np.linalg.norm(d1, axis=-1, keepdims=True)
     return tuple(torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)) for x in (k0, k1, d0, d1))

@@ -10,7 +10,8 @@ package __init__ needs cv2), loads the deterministic weights
 ``lightglue_amd.matcher.seeded_state_dict(seed, L)`` (strict: the parameter names must match),
 runs ``forward(kpts0, kpts1, desc0, desc1)`` in float32 on CPU on
 ``lightglue_amd.matcher.synthetic_pair(seed, m, n)`` and the reference ``filter_matches``
-(thresholds 0.1 and 0.0). Weights and inputs are regenerated bit-exactly from their seeds, so only the
+(thresholds 0.1 and 0.0); SWEEP_CASES do the same at the BASELINE sweep sizes on pairs with
+true correspondences and keep a row subset plus checksums. Weights and inputs are regenerated bit-exactly from their seeds, so only the
 outputs are stored (with a sha256 of the regenerated inputs + weights).
 """
 from __future__ import annotations
@@ -36,6 +37,13 @@ CASES = {
     "match_l2_64x48": (1, 2, 64, 48),
     "match_l9_120x97": (2, 9, 120, 97),
     "match_l3_300x257": (3, 3, 300, 257),
+}
+# BASELINE configs[3] sweep sizes, 9 layers, pairs with `overlap` true correspondences
+# (matcher.synthetic_pair(..., overlap)); only a row subset of the m x n log-assignment, its first
+# column and per-row / per-column sums are stored.
+# name: (seed, n_layers, m, n, overlap, row_stride)
+SWEEP_CASES = {
+    "sweep_l9_512x512": (11, 9, 512, 512, 384, 16),
 }
 
 
@@ -74,6 +82,30 @@ def main():
         print(name, {k: v.shape for k, v in out.items()}, "matches", int(matches.shape[0]))
     with open(os.path.join(HERE, "matcher_index.json"), "w") as f:
         json.dump(index, f, indent=1, sort_keys=True)
+    sweep = {}
+    for name, (seed, layers, m, n, overlap, stride) in SWEEP_CASES.items():
+        model = lg.LightGlue(features=None, n_layers=layers).eval()
+        sd = matcher.seeded_state_dict(seed, layers)
+        model.load_state_dict(sd, strict=True)
+        pair = matcher.synthetic_pair(seed, m, n, overlap=overlap)
+        with torch.no_grad():
+            d0, d1, scores = model(*pair)
+            matches, mscores = lg.filter_matches(scores, 0.1)
+            matches_all, mscores_all = lg.filter_matches(scores, 0.0)
+        sc = scores[0].numpy()
+        rows = np.arange(0, m, stride)
+        out = {"rows": rows, "scores_rows": sc[rows], "scores_col0": sc[:, 0],
+               "scores_row_sums": sc.astype(np.float64).sum(1), "scores_col_sums": sc.astype(np.float64).sum(0),
+               "desc0_rows": d0[0].numpy()[rows], "desc1_rows": d1[0].numpy()[rows],
+               "matches": matches.numpy().astype(np.int64), "mscores": mscores.numpy(),
+               "matches_all": matches_all.numpy().astype(np.int64), "mscores_all": mscores_all.numpy()}
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+        sweep[name] = {"seed": seed, "n_layers": layers, "m": m, "n": n, "overlap": overlap,
+                       "inputs_sha256": digest(sd, pair), "n_matches": int(matches.shape[0]),
+                       "n_matches_all": int(matches_all.shape[0])}
+        print(name, "matches", int(matches.shape[0]), "mutual", int(matches_all.shape[0]))
+    with open(os.path.join(HERE, "matcher_sweep_index.json"), "w") as f:
+        json.dump(sweep, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":

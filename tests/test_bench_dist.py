@@ -29,7 +29,7 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ws, r, local = bench.dist_env()
     assert (ws, r, local) == (world, rank, rank)
-    barrier, reduce_max = bench.make_collectives(torch, dist, torch.device("cpu"))
+    barrier, reduce_max = bench.make_collectives(torch, dist)
     # rank 1 is slower: the reported time must be the max over ranks
     dt = bench.timed_region(lambda: time.sleep(0.05 + 0.1 * rank), barrier, lambda: None, reduce_max)
     q.put((rank, dt))
@@ -54,9 +54,73 @@ def test_timed_region_reports_max_over_ranks():
 def test_single_process_collectives_are_identity():
     import bench
 
-    barrier, reduce_max = bench.make_collectives(torch, None, torch.device("cpu"))
+    barrier, reduce_max = bench.make_collectives(torch, None)
     barrier()
     assert reduce_max(1.5) == 1.5
+    assert bench.gather(None, "x") == ["x"]
+
+
+_RANK_SCRIPT = r"""
+import os, sys, torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+import bench
+ws, rank, local = bench.dist_env()
+assert ws == 2 and rank == local and os.environ["MASTER_ADDR"] == "127.0.0.1", (ws, rank, local)
+dist.init_process_group("gloo")
+got = bench.gather(dist, rank * 10)
+assert got == [0, 10], got
+dist.destroy_process_group()
+sys.exit(int(sys.argv[2]) if rank == 1 else 0)
+"""
+
+
+def test_launcher_starts_one_rank_per_gpu(tmp_path):
+    """bench.py --gpus N outside torchrun: N rank processes with RANK/LOCAL_RANK/WORLD_SIZE and a
+    127.0.0.1 rendezvous, gloo group, exit status propagated."""
+    import sys
+
+    import bench
+
+    script = tmp_path / "rank.py"
+    script.write_text(_RANK_SCRIPT)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env_ws = os.environ.pop("WORLD_SIZE", None)
+    try:
+        assert bench.launch_replicas(2, [repo, "0"], count_devices=lambda: 2, script=str(script)) == 0
+        assert bench.launch_replicas(2, [repo, "3"], count_devices=lambda: 2, script=str(script)) == 3
+    finally:
+        if env_ws is not None:
+            os.environ["WORLD_SIZE"] = env_ws
+
+
+def test_launcher_refuses_missing_devices(capsys):
+    import bench
+
+    assert bench.launch_replicas(8, [], count_devices=lambda: 1) == 2
+    assert "--gpus 8 needs 8 visible GPUs, found 1" in capsys.readouterr().err
+
+
+def test_bench_gpus2_fails_loudly_without_devices():
+    """The driver's `python bench.py --gpus 2` on a box with fewer GPUs exits non-zero with a message."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("this host has >= 2 GPUs")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--quick"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2
+    assert "--gpus 2 needs 2 visible GPUs" in r.stderr
+
+
+def test_cpu_share_respects_quota(monkeypatch):
+    import bench
+
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    use, aff, _ = bench.cpu_share()
+    assert use == min(3, aff)
 
 
 def test_work_accounting():
