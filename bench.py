@@ -353,38 +353,44 @@ def variants(torch, lightglue_amd, device, stream, q, k, v, flops):
 def concurrent_streams(torch, lightglue_amd, device, nq, nkv, rank, flops, per_stream=500):
     """Independent calls of the metric shape issued on S streams at once (S image pairs in flight,
     each stream its own Q/K/V/O and its own graph of `per_stream` dependent enqueues): whole-GPU
-    calls/s. The single call occupies 128 of the 256 CUs, so two streams overlap completely."""
+    calls/s. Without a hint a call fills all 256 CUs (16-row blocks), so streams barely overlap;
+    with the concurrency hint set to S (mha_hd64_set_concurrency_hint) the planner gives each call
+    32-row blocks on half the CUs (S = 2) or in the two-per-CU form (S >= 3)."""
     from lightglue_amd import synth
 
     out = {}
     for S in (2, 4):
-        streams = [torch.cuda.Stream(device) for _ in range(S)]
-        graphs = []
-        for i, st in enumerate(streams):
-            qn, kn, vn = synth.qkv(500 + 17 * rank + i, nq, nkv)
-            q, k, v = (torch.from_numpy(x).to(device).half().contiguous() for x in (qn, kn, vn))
-            o = torch.empty_like(q)
-            with torch.cuda.stream(st):
-                lightglue_amd.mha_hd64(q, k, v, out=o)  # per-stream workspace, outside capture
-                torch.cuda.synchronize(device)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=st):
-                    for _ in range(per_stream):
-                        lightglue_amd.mha_hd64(q, k, v, out=o)
-            graphs.append((g, st, (q, k, v, o)))
-        for g, st, _ in graphs:  # warm
-            with torch.cuda.stream(st):
-                g.replay()
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        for g, st, _ in graphs:
-            with torch.cuda.stream(st):
-                g.replay()
-        torch.cuda.synchronize(device)
-        dt = time.perf_counter() - t0
-        calls = S * per_stream
-        out[str(S)] = {"calls_per_s": round(calls / dt, 1), "us_per_call": round(dt * 1e6 / calls, 3),
-                       "tflops": round(calls * flops / dt / 1e12, 2)}
+        for hinted in (False, True):
+            prev = lightglue_amd.set_concurrency_hint(S if hinted else 1)
+            streams = [torch.cuda.Stream(device) for _ in range(S)]
+            graphs = []
+            for i, st in enumerate(streams):
+                qn, kn, vn = synth.qkv(500 + 17 * rank + i, nq, nkv)
+                q, k, v = (torch.from_numpy(x).to(device).half().contiguous() for x in (qn, kn, vn))
+                o = torch.empty_like(q)
+                with torch.cuda.stream(st):
+                    lightglue_amd.mha_hd64(q, k, v, out=o)  # per-stream workspace, outside capture
+                    torch.cuda.synchronize(device)
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=st):
+                        for _ in range(per_stream):
+                            lightglue_amd.mha_hd64(q, k, v, out=o)
+                graphs.append((g, st, (q, k, v, o)))
+            lightglue_amd.set_concurrency_hint(prev)
+            for g, st, _ in graphs:  # warm
+                with torch.cuda.stream(st):
+                    g.replay()
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            for g, st, _ in graphs:
+                with torch.cuda.stream(st):
+                    g.replay()
+            torch.cuda.synchronize(device)
+            dt = time.perf_counter() - t0
+            calls = S * per_stream
+            out[f"{S}" + ("_hinted" if hinted else "")] = {
+                "calls_per_s": round(calls / dt, 1), "us_per_call": round(dt * 1e6 / calls, 3),
+                "tflops": round(calls * flops / dt / 1e12, 2)}
     return out
 
 

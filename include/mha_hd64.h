@@ -195,6 +195,17 @@ int32_t mha_hd64_launch_grouped(const mha_hd64_call_t* calls, int32_t n_calls, i
 /* Workspace bytes the grouped launcher can use (0 = no call of the group splits). */
 size_t mha_hd64_grouped_workspace_bytes(const mha_hd64_call_t* calls, int32_t n_calls);
 
+/* ---- concurrency hint (no reference counterpart: TensorRT gives a plugin no view of its
+ * other streams) ----
+ * How many independent enqueue streams the host keeps busy on this process's GPUs at once
+ * (independent image pairs, one stream each). 1 (default): every call
+ * may take the whole chip, so a 1x4x1024x1024 call runs on 256 workgroups of 16 query rows, one
+ * per CU. 2: calls take half the chip (128 workgroups of 32 rows) so two streams' calls run side
+ * by side. >= 3: the same 32-row blocks in the two-per-CU form (65 KiB of LDS each), so up to
+ * four calls share the chip. Results are identical in every mode up to fp32 summation order
+ * (each mode is deterministic). Returns the previous hint; values < 1 read as 1. Process-wide. */
+int32_t mha_hd64_set_concurrency_hint(int32_t streams);
+
 /* ---- diagnostics ---- */
 const char* mha_hd64_last_error(void);           /* thread-local message of the last failure   */
 void        mha_hd64_set_abort_on_error(int32_t enable); /* 1 = abort() like PLUGIN_ASSERT     */

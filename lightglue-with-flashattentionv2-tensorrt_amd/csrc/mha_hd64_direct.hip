@@ -580,9 +580,12 @@ hipError_t launch_direct(const FwdArgs& a, int grid, int tiles_per_wave, bool ou
         const char* e = std::getenv("MHA_HD64_DIRECT_SHARED");
         return !(e && e[0] == '0');
     }();
-    if (tiles_per_wave == 2 && grid > 256 && four && shared)
+    // (a concurrency hint >= 3 takes the two-per-CU form at any grid: each call then leaves room for
+    // other streams' calls on the same CUs)
+    const bool many = grid > 256 || concurrency_hint() >= 3;
+    if (tiles_per_wave == 2 && many && four && shared)
         return out_f32 ? launch_direct_t<float, 4, 2, 2>(a, grid, stream) : launch_direct_t<f16, 4, 2, 2>(a, grid, stream);
-    if (tiles_per_wave > 2 && grid > 256 && four && shared)  // nkv in (1024, 2048], the same: 4 passes of 2
+    if (tiles_per_wave > 2 && many && four && shared)  // nkv in (1024, 2048], the same: 4 passes of 2
         return out_f32 ? launch_direct_t<float, 4, 2, 4>(a, grid, stream) : launch_direct_t<f16, 4, 2, 4>(a, grid, stream);
     if (tiles_per_wave > 2) {
         if (four)

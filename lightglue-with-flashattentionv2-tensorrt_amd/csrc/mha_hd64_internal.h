@@ -86,5 +86,8 @@ void set_stamp_buffer(void* p);
 void set_fused_combine(int enable);
 // How the calling thread's last launch merged its splits: 0 none, 1 in-launch, 2 combine kernel.
 int last_combine_form();
+// Concurrent enqueue streams the host keeps busy (mha_hd64_set_concurrency_hint); >= 1.
+int concurrency_hint();
+int set_concurrency_hint(int streams);
 
 }  // namespace mha_hd64

@@ -37,6 +37,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -911,6 +912,12 @@ constexpr int kArenaTickets = 1 << 20;  // 4 MiB per device
 
 int last_combine_form() { return g_last_combine; }
 
+namespace {
+std::atomic<int> g_concurrency{1};
+}
+int concurrency_hint() { return g_concurrency.load(std::memory_order_relaxed); }
+int set_concurrency_hint(int streams) { return g_concurrency.exchange(std::max(1, streams)); }
+
 void set_fused_combine(int enable) {
     std::lock_guard<std::mutex> lk(g_ticket_mu);
     g_fused = enable ? 1 : 0;
@@ -1032,8 +1039,11 @@ static bool direct16_enabled() {
 GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_waves, int force_kv_waves,
                      int force_splits, InType in) {
     GroupPlan p{};
-    // 16-row blocks first: a launch of at most 256 of them runs every block on its own CU
-    if (force_q_waves == kForceDirect16 || (force_q_waves == 0 && direct16_enabled())) {
+    // 16-row blocks first: a launch of at most 256 of them runs every block on its own CU. Under a
+    // concurrency hint >= 2 (several streams of independent calls) a call takes 32-row blocks on
+    // half the CUs instead (launch_direct: two-per-CU form from hint 3), so the streams overlap.
+    if (force_q_waves == kForceDirect16 ||
+        (force_q_waves == 0 && direct16_enabled() && concurrency_hint() < 2)) {
         const int dt = direct_tiles_for(calls, n, in, force_q_waves == kForceDirect16, 16);
         if (dt > 0) {
             p.q_waves = 1;

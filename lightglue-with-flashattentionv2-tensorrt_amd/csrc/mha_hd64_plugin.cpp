@@ -353,6 +353,7 @@ size_t mha_hd64_grouped_workspace_bytes(const mha_hd64_call_t* calls, int32_t n_
 // ---- diagnostics ----
 const char* mha_hd64_last_error(void) { return g_last_error.c_str(); }
 void mha_hd64_set_abort_on_error(int32_t enable) { g_abort_on_error = enable != 0; }
+int32_t mha_hd64_set_concurrency_hint(int32_t streams) { return mha_hd64::set_concurrency_hint(streams); }
 const char* mha_hd64_build_info(void) {
     return "mha_hd64: gfx950 (CDNA4) HIP kernels, v_mfma_f32_32x32x16_f16 + ds_read_b64_tr_b16; "
            "variants fp16->fp16, fp16->fp32, fp32->fp32; single-pass kernel (32 rows x all keys per workgroup, K/V by LDS-DMA) "

@@ -12,6 +12,7 @@ from .plugin import (  # noqa: F401
     mha_hd64,
     mha_hd64_batched,
     mha_hd64_grouped,
+    set_concurrency_hint,
 )
 from . import ops  # noqa: F401,E402  (registers torch.ops.lightglue_amd.*)
 
@@ -24,6 +25,7 @@ __all__ = [
     "mha_hd64",
     "mha_hd64_batched",
     "mha_hd64_grouped",
+    "set_concurrency_hint",
     "load_library",
     "LIB_PATH",
 ]

@@ -225,6 +225,14 @@ def _workspace(device: torch.device, stream: int, nbytes: int) -> torch.Tensor:
     return ws
 
 
+def set_concurrency_hint(streams: int) -> int:
+    """Tell the planner how many independent enqueue streams are kept busy at once (C ABI
+    mha_hd64_set_concurrency_hint): 1 = every call may fill the chip; 2 = calls take half the CUs
+    so two streams overlap; >= 3 = half-LDS two-per-CU blocks so up to four share the chip.
+    Process-wide; returns the previous value."""
+    return int(_lib.load().mha_hd64_set_concurrency_hint(int(streams)))
+
+
 def _require_gpu(*ts: torch.Tensor) -> None:
     for t in ts:
         if not t.is_cuda:

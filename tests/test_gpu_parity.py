@@ -842,3 +842,33 @@ def test_nan_inputs_propagate_like_the_reference(where, n, dev):
         o = mha_hd64(*(_t(a, dev, dt) for a in (qn, kn, vn)))
         torch.cuda.synchronize()
         assert torch.equal(torch.isnan(o.float().cpu()), torch.isnan(ref)), (where, dt)
+
+
+@pytest.mark.parametrize("hint", [2, 3, 4])
+@pytest.mark.parametrize("nq,nkv", [(1024, 1024), (1000, 777), (512, 2048), (100, 100)])
+def test_concurrency_hint_plans_match_oracle(hint, nq, nkv, dev, oracle_mod):
+    """mha_hd64_set_concurrency_hint(>= 2): single calls take 32-row blocks (half the CUs; the
+    two-per-CU form from 3) so independent streams overlap; same results within the contract."""
+    import ctypes
+
+    import lightglue_amd
+    from lightglue_amd import _lib, mha_hd64, synth
+
+    qn, kn, vn = synth.qkv(777 + nq + nkv, nq, nkv)
+    q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
+    ref = oracle_mod.attention_c(q16, k16, v16)
+    q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+    prev = lightglue_amd.set_concurrency_hint(hint)
+    try:
+        plan = (ctypes.c_int32 * 4)()
+        _lib.load().mha_hd64_plan(1, 4, nq, nkv, 5242880, plan)
+        assert plan[0] != 22  # never the whole-chip 16-row kernel under the hint
+        a = mha_hd64(q, k, v)
+        b = mha_hd64(q, k, v)
+        torch.cuda.synchronize()
+    finally:
+        lightglue_amd.set_concurrency_hint(prev)
+    got = a.float().cpu().numpy()
+    assert torch.equal(a, b)
+    assert _maxdiff(got, ref) <= TOL
+    _regress16(got, ref)
