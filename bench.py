@@ -84,7 +84,7 @@ def launch_replicas(n, argv, count_devices=visible_devices, python=sys.executabl
     import subprocess
 
     have = count_devices()
-    if have < n:
+    if have < n and os.environ.get("BENCH_SHARE_DEVICE") != "1":
         print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}", file=sys.stderr, flush=True)
         return 2
     port = str(_free_port())
@@ -558,11 +558,14 @@ def main():
     if ws != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr, flush=True)
         sys.exit(2)
-    if visible_devices() <= local:
+    # BENCH_SHARE_DEVICE=1 (rehearsal only): ranks share the visible GPUs round-robin, so the N>1
+    # path (gloo group, gathers, per-rank lines) can run on a one-GPU box; a real run never sets it
+    share = os.environ.get("BENCH_SHARE_DEVICE") == "1"
+    if visible_devices() <= local and not share:
         print(f"bench.py: rank {rank} needs GPU {local}, {visible_devices()} visible", file=sys.stderr, flush=True)
         sys.exit(2)
     dist = None
-    device = torch.device("cuda", local)
+    device = torch.device("cuda", local % max(1, visible_devices()) if share else local)
     torch.cuda.set_device(device)
     if ws > 1:
         import torch.distributed as dist
@@ -761,15 +764,28 @@ def main():
             "tflops": round(B * flops / (tb * 1e-3) / 1e12, 2),
             "frac": round(B * flops / (tb * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
         }
+        # more calls per launch (a pair stream of 16 / 32 pairs' calls stacked): the planner's plan,
+        # graph replay of 50 back-to-back launches
+        sweep_b = {}
+        for B2 in (16, 32):
+            qs, ks, vs = (torch.from_numpy(x).to(device).half().contiguous()
+                          for x in synth.qkv(310 + B2 + rank, nq, nkv, batch=B2))
+            os_ = torch.empty_like(qs)
+            t2 = graph_per_launch_ms(torch, lambda: lightglue_amd.mha_hd64_batched(qs, ks, vs, out=os_), stream, k=50)
+            sweep_b[str(B2)] = {"launch_us": round(t2 * 1e3, 3), "calls_per_s_per_gpu": round(B2 / (t2 * 1e-3), 1),
+                                "frac": round(B2 * flops / (t2 * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4)}
+            del qs, ks, vs, os_
+        result["batched"]["more_calls_per_launch"] = sweep_b
+        best_b, best = max(((B, result["batched"]["frac"]),) + tuple((int(b), v["frac"]) for b, v in sweep_b.items()),
+                           key=lambda x: x[1])
 
         # The 70 % bar read against the saturated form: one call alone is bounded by the dependent
         # launch boundary (MI355X_MICROARCH.md price list, row 'boundary': 1.45 us between trivial
         # 256-workgroup kernels) against an ideal 0.43 us of MFMA work.
         result["roofline"]["ideal_us_at_peak"] = round(flops / (PEAK_F16_TFLOPS * 1e12) * 1e6, 4)
         result["roofline"]["launch_boundary_floor_us"] = 1.45
-        result["roofline"]["saturated"] = {"form": f"{B} calls per launch (batched)",
-                                           "frac": result["batched"]["frac"],
-                                           "tflops": result["batched"]["tflops"]}
+        result["roofline"]["saturated"] = {"form": f"{best_b} calls per launch (batched), best of 8 / 16 / 32",
+                                           "frac": best, "frac_8_calls": result["batched"]["frac"]}
 
         result["variants"] = variants(torch, lightglue_amd, device, stream, q, k, v, flops)
         result["concurrent_streams"] = concurrent_streams(torch, lightglue_amd, device, nq, nkv, rank, flops)

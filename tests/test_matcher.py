@@ -253,9 +253,10 @@ SWEEP = json.load(open(os.path.join(GOLD, "matcher_sweep_index.json")))
 # fp16 path at 9 layers (weights, activations and attention in fp16): log-scores are sums of two
 # log-softmaxes over 512 entries of a similarity built from fp16 descriptors; an fp16 descriptor
 # error e moves a similarity by ~|d| e, and both softmax normalisers by a weighted mean of such
-# moves, so per-element errors stay near the descriptor error times the similarity scale. The bounds
-# below are ~3x the MI355X observation (tests print it); fp32 models keep the fp32 bounds above.
-SWEEP_TOL = {"float32": (TOL_DESC32, TOL_SCORE32, 1e-3), "float16": (TOL_DESC16, TOL_SCORE16, 5e-3)}
+# moves, so per-element errors stay near the descriptor error times the similarity scale. Observed on
+# MI355X (the test prints them): fp32 3.2e-3 / 2.6e-2 / 1.3e-4, fp16 1.8e-2 / 0.22 / 1.1e-3
+# (descriptors / log-scores / relative row and column sums); bounds ~3-4x those.
+SWEEP_TOL = {"float32": (1e-2, 1e-1, 5e-4), "float16": (6e-2, 0.6, 5e-3)}
 SWEEP_RECALL = 0.9
 
 
