@@ -129,3 +129,16 @@ def test_work_accounting():
     assert bench.call_flops(1, 4, 1024, 1024) == 1073741824
     assert bench.call_bytes(1, 4, 1024, 1024) == 2097152
     assert bench.call_bytes(1, 4, 1024, 1024, out_bytes=4) == 2621440
+
+
+def test_bench_refuses_world_size_mismatch():
+    """Under a torchrun environment, --gpus must equal WORLD_SIZE (checked before any GPU call)."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29555")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "1", "--quick"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2
+    assert "--gpus 1 but WORLD_SIZE=2" in r.stderr
