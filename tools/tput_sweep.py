@@ -33,7 +33,9 @@ for case in cases:
                                               nkv, 0, 0, 0, 0, 0, ws.data_ptr(), ws.numel(), stream.cuda_stream, 3)
     bench.graph_per_launch_ms(torch, warm, stream, k=400, reps=5)
     shapes = [("planner_first", 0, 0), ("ring42", 4, 2), ("ring41", 4, 1)]
-    shapes += [(f"ring{x}", int(x[0]), int(x[1])) for x in os.environ.get("EXTRA_SHAPES", "").split(",") if x]
+    # EXTRA_SHAPES="q-k,...": forced (q_waves, kv_waves) codes, e.g. 12-2 = (2,2) with 64-row waves
+    shapes += [(f"ring{x}", int(x.split("-")[0]), int(x.split("-")[1]))
+               for x in os.environ.get("EXTRA_SHAPES", "").split(",") if x]
     for name, qw, kw in shapes + [("planner", 0, 0)]:
         def run():
             return lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), b, 4, nq, nkv,
