@@ -546,6 +546,52 @@ def matcher_e2e(torch, device, stream, rank, sizes=(512, 1024, 2048), reps=10):
     return res
 
 
+def matcher_pair_streams(torch, lightglue_amd, device, rank, n=1024, streams=(1, 2, 4, 8), reps=10):
+    """BASELINE configs[4] on one GPU: a stream of independent image pairs through the end-to-end
+    fp16 matcher, S pairs in flight (S streams, each replaying its own captured forward; the
+    concurrency hint set to S while capturing, so each attention call leaves room for the other
+    streams). Whole-GPU pairs/s (host clock around all streams, best of `reps` rounds)."""
+    from lightglue_amd import matcher
+
+    model = matcher.LightGlueMatcher(n_layers=9).eval()
+    model.load_state_dict(matcher.seeded_state_dict(7, 9), strict=True)
+    model = model.to(device, torch.float16)
+    res = {}
+    for S in streams:
+        prev = lightglue_amd.set_concurrency_hint(S)
+        try:
+            graphs = []
+            for i in range(S):
+                st = torch.cuda.Stream(device)
+                pair = tuple(t.to(device, torch.float16) for t in matcher.synthetic_pair(60 + 7 * rank + i, n, n))
+                with torch.no_grad():
+                    with torch.cuda.stream(st):
+                        for _ in range(2):
+                            model(*pair)  # warm: this stream's workspace + allocator outside the capture
+                    st.synchronize()
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=st):
+                        out = model(*pair)
+                graphs.append((g, st, pair, out))
+        finally:
+            lightglue_amd.set_concurrency_hint(prev)
+        best = None
+        for rep in range(reps + 1):
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            for g, st, _, _ in graphs:
+                with torch.cuda.stream(st):
+                    g.replay()
+            torch.cuda.synchronize(device)
+            dt = time.perf_counter() - t0
+            if rep:
+                best = dt if best is None else min(best, dt)
+        assert all(bool(torch.isfinite(o[2]).all()) for _, _, _, o in graphs)
+        res[str(S)] = {"pairs_per_s": round(S / best, 1), "ms_per_round": round(best * 1e3, 4)}
+        del graphs
+    return res
+
+
 def profile_driver(torch, args, device):
     """Eager launches of one workload (for rocprofv3 --kernel-trace / --pmc passes)."""
     import lightglue_amd
@@ -832,12 +878,18 @@ def main():
         result["concurrent_streams"] = concurrent_streams(torch, lightglue_amd, device, nq, nkv, rank, flops)
         result["matcher_attention"] = matcher_attention(torch, device, stream, rank, separate=args.matcher_separate)
         result["matcher_e2e_fp16"] = matcher_e2e(torch, device, stream, rank)
+        result["matcher_pair_streams_fp16"] = {"n": nq, "streams": matcher_pair_streams(torch, lightglue_amd, device,
+                                                                                        rank, n=nq)}
         # whole-job pair rate (BASELINE configs[4]): each GPU streams its own pairs through the matcher
         pair_rates = gather(dist, result["matcher_e2e_fp16"][str(nq)]["pairs_per_s"]
                             if str(nq) in result["matcher_e2e_fp16"] else None)
+        stream_rates = gather(dist, max(v["pairs_per_s"] for v in
+                                        result["matcher_pair_streams_fp16"]["streams"].values()))
         if all(p is not None for p in pair_rates):
             result["pairs_per_s_all_gpus"] = {"matcher_e2e_fp16": round(sum(pair_rates), 1), "n": nq,
-                                              "per_rank": pair_rates}
+                                              "per_rank": pair_rates,
+                                              "pair_streams_best": round(sum(stream_rates), 1),
+                                              "pair_streams_per_rank": stream_rates}
 
     if args.sweep and rank == 0:
         sweep(torch, lib, device, stream, nq, nkv)
