@@ -429,6 +429,34 @@ def overlapped_batched(torch, lightglue_amd, device, nq, nkv, rank, flops, B=16,
             "tflops": round(calls * flops / best / 1e12, 2), "frac": round(calls * flops / best / 1e12 / PEAK_F16_TFLOPS, 4)}
 
 
+def cold_inputs(torch, lightglue_amd, stream, q, k, v, barrier, reduce_max, ws, pool_mib=640):
+    """The headline's calls again, each on its own copy of Q/K/V from a pool larger than every cache.
+
+    The headline re-reads one Q/K/V, and an XCD's L2 keeps a launch's lines for the next launch on
+    the stream (tools/mb_l2_retention.hip: a dependent load costs 220 cycles in the next launch,
+    740 after a 256 MiB scrub; profiles/r02/l2_retention.txt). Here consecutive calls read
+    different buffers and a buffer comes round again only after pool_mib MiB (> the 256 MiB MALL +
+    8 x 4 MiB L2), so every call fetches its inputs from HBM: what a producer that streams fresh
+    pairs through the plugin sees when its Q/K/V are no longer in any cache."""
+    per_set = 3 * q.numel() * q.element_size()
+    sets = max(2, -(-(pool_mib << 20) // per_set))
+    pool = [(q.clone(), k.clone(), v.clone(), torch.empty_like(q)) for _ in range(sets)]
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=stream):
+        for (a, b, c, o) in pool:
+            lightglue_amd.mha_hd64(a, b, c, out=o)
+    graph.replay()
+    stream.synchronize()
+    ok = all(torch.equal(o, pool[0][3]) for (_, _, _, o) in pool[1:])
+    elapsed, _ = timed_replays(torch, graph.replay, stream, barrier, reduce_max, 5)
+    del graph, pool
+    return {"calls_per_graph": sets, "pool_mib": round(sets * per_set / 2**20, 1),
+            "calls_per_s": round(sets * ws / elapsed, 1), "us_per_call": round(elapsed / sets * 1e6, 3),
+            "outputs_identical_to_each_other": ok,
+            "how": "each call on its own copy of the headline's Q/K/V (pool larger than MALL + L2), one graph of "
+                   "all calls, median of 5 replays"}
+
+
 def sweep(torch, lib, device, stream, nq, nkv):
     """Main-kernel (+combine) time for every compiled workgroup shape and KV split, single call and
     batched; one JSON object per line on stderr (tuning aid for plan_call)."""
@@ -821,6 +849,7 @@ def main():
             "flops_per_launch": flops, "algorithmic_bytes_per_call": call_bytes(1, 4, nq, nkv),
         }
         result["isolated_call_us"] = round(t_call * 1e3, 3)
+        result["cold_inputs"] = cold_inputs(torch, lightglue_amd, stream, q, k, v, barrier, reduce_max, ws)
 
         # Batched launch: `batched` independent calls stacked in the batch dimension of one launch.
         B = args.batched
