@@ -224,6 +224,42 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
 }
+
+// L2 prefetch for the single-pass kernels (issued by one wave per workgroup, before its own
+// loads). A workgroup's DMA requests K of its first tiles at entry but V tile by tile once K(t)
+// is in registers, and the later K tiles once K(0) has landed, so with inputs not already in the
+// L2 those requests wait a second memory round trip. The `group` workgroups of one (batch, head)
+// that the XCD-aware order puts on one XCD (consecutive query tiles) split that head's rows:
+// workgroup r (= qtile % group) touches rows r + group·i, one dword per 128-B row, V always and K
+// where the DMA asks late (row % WAVE_KEYS >= EARLY_KEYS). Only the fill matters (every row must
+// be touched: every other row gains nothing, profiles/r02/prefetch_ab.txt); the returned dwords
+// are kept live until the caller's first wait covers them (oldest loads of the wave). Masked
+// lanes rather than out-of-range offsets: a full-wave load costs warm-input calls more.
+struct L2Prefetch {
+    unsigned k[2] = {0u, 0u}, v[2] = {0u, 0u};
+};
+// workgroups of one (batch, head) per XCD in the XCD-aware order (0: too few to split the rows)
+__device__ __forceinline__ int prefetch_group(int total_blocks, int qtiles) {
+    const int n = min(total_blocks >> 3, qtiles);
+    return n >= 32 ? 32 : (n >= 16 ? 16 : 0);
+}
+template <int WAVE_KEYS, int EARLY_KEYS>
+__device__ __forceinline__ void l2_prefetch(L2Prefetch& pf, __amdgpu_buffer_rsrc_t k_rs, __amdgpu_buffer_rsrc_t v_rs,
+                                            int nkv, int qtile, int group, int lane) {
+    if (group == 0) return;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {  // nkv <= 2048: at most 128 rows per workgroup
+        if (group * 64 * c >= nkv) break;
+        const int row = (qtile & (group - 1)) + group * (lane + 64 * c);
+        const unsigned off = (unsigned)row * 128u;
+        if (EARLY_KEYS < WAVE_KEYS && row < nkv && row % WAVE_KEYS >= EARLY_KEYS)
+            asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(pf.k[c]) : "v"(off), "s"(k_rs));
+        if (row < nkv) asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(pf.v[c]) : "v"(off), "s"(v_rs));
+    }
+}
+__device__ __forceinline__ void l2_prefetch_done(L2Prefetch& pf) {
+    asm volatile("" : "+v"(pf.k[0]), "+v"(pf.k[1]), "+v"(pf.v[0]), "+v"(pf.v[1])::"memory");
+}
 // 8 consecutive output values (dims c8..c8+7 of one row) as one (f16) or two (f32) 16-B stores.
 template <typename T, int AUX>
 __device__ __forceinline__ void store8(__amdgpu_buffer_rsrc_t rs, unsigned voff, f32x4 a, f32x4 b) {

@@ -190,6 +190,17 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         // through the wave's two 8 KiB slots: tile t's V is issued into slot t as soon as K(t)'s
         // fragments are in registers, so K(1) lands under QKᵀ(0) and V under all of the scores.
         f16x8 qraw[4];
+        // K(0) and K(1) first: the first tile's K is not queued behind the whole wave's K
+        constexpr int KFIRST = TPW < 2 ? TPW : 2;
+#ifndef MHA_D_PREFETCH
+#define MHA_D_PREFETCH 1  // 0: no L2 prefetch (A/B hook)
+#endif
+        // L2 prefetch of the rows requested late (mha_hd64_device.h; profiles/r02/prefetch_ab.txt)
+        L2Prefetch pf;
+        if constexpr (MHA_D_PREFETCH != 0 && !(MHA_ABL & ABL_NO_GLOAD))
+            if (wave == 0)
+                l2_prefetch<WAVE_KEYS, kTileKV * KFIRST>(pf, k_rs, v_rs, nkv, qtile,
+                                                         prefetch_group(a.total_blocks, ca.qtiles), lane);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             if (MHA_ABL & ABL_NO_GLOAD) qraw[s] = f16x8{} + (f16)(lane * 0.01f);
@@ -197,12 +208,11 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
                               : "=v"(qraw[s])
                               : "v"((unsigned)(q_row * kHeadDim + 16 * s + 8 * hh) * 2), "s"(q_rs));
         }
-        // K(0) and K(1) first: the first tile's K is not queued behind the whole wave's K
-        constexpr int KFIRST = TPW < 2 ? TPW : 2;
         dma_k(0, KFIRST);
         // Q and K(0) have landed (issue order: Q, K(0), K(1), 8 pieces per tile)
         wait_vm<8 * (KFIRST - 1)>();
         asm volatile("" : "+v"(qraw[0]), "+v"(qraw[1]), "+v"(qraw[2]), "+v"(qraw[3])::"memory");
+        l2_prefetch_done(pf);  // older than Q
         DSTAMP(1);
         // the rest of K; every later K(t) wait sees K(t+1..) and V(0..t-1) younger: vmcnt(8*(TPW-1))
         dma_k(KFIRST, TPW);

@@ -212,6 +212,17 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         // K(0)'s DMA ahead of the Q loads (same wait counts) for the 2-tile form: 1x4x512^2 3.36-3.40
         // vs 3.42-3.52 us; the 4-tile form (the metric call) keeps Q first (4.97-5.04 vs 4.89-4.99)
         constexpr bool K0F = MHA_D16_K0_FIRST || (TPW == 2 && PASSES == 1);
+#ifndef MHA_D16_PREFETCH
+#define MHA_D16_PREFETCH 1  // 0: no L2 prefetch (A/B hook)
+#endif
+        // L2 prefetch of the rows requested late (mha_hd64_device.h). Measured at 1x4x1024^2
+        // (tools/cold_probe.py, profiles/r02/prefetch_ab.txt): inputs from HBM 6.72 -> 5.7 us,
+        // L2-resident inputs +0.02 us (4.65); at 768^2 / 1024x2048 -15 / -22 % cold, +2 % warm.
+        L2Prefetch pf;
+        if constexpr (MHA_D16_PREFETCH != 0)
+            if (wave == 0)
+                l2_prefetch<WAVE_KEYS, 2 * kTileKV>(pf, k_rs, v_rs, nkv, qtile,  // K(0), K(1) at entry
+                                                    prefetch_group(total_blocks, ca.qtiles), lane);
         if constexpr (K0F) dma_k(0, 1);
 #pragma unroll
         for (int s = 0; s < 2; ++s)
@@ -219,8 +230,9 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
                          : "=v"(qraw[s])
                          : "v"((unsigned)(q_row * kHeadDim + 32 * s + 8 * g) * 2), "s"(q_rs));
         dma_k(K0F ? 1 : 0, 2);
-        wait_vmc<8>();  // Q and K(0) landed (younger: K(1))
+        wait_vmc<8>();  // Q and K(0) landed (younger: K(1)); the prefetch too
         asm volatile("" : "+v"(qraw[0]), "+v"(qraw[1])::"memory");
+        l2_prefetch_done(pf);
         DSTAMP(1);
         dma_k(2, TPW);
         {
