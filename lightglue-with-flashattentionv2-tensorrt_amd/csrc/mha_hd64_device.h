@@ -57,7 +57,9 @@ struct FwdArgs {
 // Single-pass kernel (mha_hd64_direct.hip): 8 waves x tiles_per_wave 64-key tiles per 32-row block.
 hipError_t launch_direct(const FwdArgs& a, int grid, int tiles_per_wave, bool out_f32, hipStream_t stream);
 // 16-row single-pass kernel (mha_hd64_direct16.hip): 4 waves x 2*tiles_per_wave 64-key tiles.
-hipError_t launch_direct16(const FwdArgs& a, int grid, int tiles_per_wave, bool out_f32, hipStream_t stream);
+// in_f32: fp32 Q/K/V rounded to fp16 inside the kernel (tiles_per_wave <= 2 only).
+hipError_t launch_direct16(const FwdArgs& a, int grid, int tiles_per_wave, bool out_f32, hipStream_t stream,
+                           bool in_f32 = false);
 
 namespace {
 // Uniform (scalar) selection of call ci's arguments from the kernarg table (grouped launches).

@@ -95,7 +95,7 @@ __device__ __forceinline__ float max16(const f32x4 (&c)[4]) {
 // PASSES = 2 (nkv in (1024, 2048], 4 waves): each wave's 2·TPW tiles go through its TPW slots twice,
 // as in mha_hd64_direct.hip's two-pass form (pass 1's K(TPW + t) refills slot t once pass 0's PV
 // has V(t)'s fragments in registers).
-template <typename TOut, int KW, int TPW, bool MULTI, int PASSES = 1>
+template <typename TOut, int KW, int TPW, bool MULTI, int PASSES = 1, bool F32IN = false>
 // The single call's own arguments come first as plain scalars (q0 .. qtiles0: 12 dwords), so the
 // command processor can preload them into SGPRs (-amdgpu-kernarg-preload-count, Makefile) and the
 // first loads need no dependent kernarg fetch; grouped launches (MULTI) read the table `a`.
@@ -104,6 +104,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
                                                                         int qtiles0, FwdArgs a) {
     static_assert(TPW >= 2 && TPW <= 4 && (KW == 4 || KW == 8), "waves x tiles per wave");
     static_assert(PASSES == 1 || (PASSES == 2 && TPW == 4 && KW == 4), "two passes: 4 waves x 2 x 4 tiles");
+    static_assert(!F32IN || (PASSES == 1 && KW == 4), "fp32 inputs: the one-pass 4-wave forms");
     constexpr int BLOCK_M = 16;                     // query rows per workgroup
     constexpr int WAVE_KEYS = kTileKV * TPW * PASSES;
     constexpr int OROW = 68;                        // epilogue fp32 row pitch
@@ -170,6 +171,161 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
 #pragma unroll
         for (int db = 0; db < 4; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
         l_acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else if constexpr (F32IN) {
+        // ---- the Float boundary inside the kernel: fp32 Q/K/V through VGPRs ----
+        // fp32 rows are 256 B. Lane L of piece i (rows 8i..8i+7 of a tile) loads the 8 floats of
+        // chunk c = L & 7 of row 8i + L/8, rounds them to fp16 (RNE, as the reference's convert
+        // kernel …fp16in_fp32out.cu:706-768) and writes the 16-B chunk where the K / V image puts
+        // it (the same images as the DMA path). Tiles in the order K(0..TPW-1), V(0..TPW-1), two
+        // in flight; tile j goes into slot j % TPW once that slot's K fragments are in registers.
+        // Loads are plain (compiler-tracked) buffer loads: no hand-counted waits in this form.
+        const float* Qf = reinterpret_cast<const float*>(ca.q) + (size_t)bh * nq * kHeadDim;
+        const float* Kf = reinterpret_cast<const float*>(ca.k) + (size_t)bh * nkv * kHeadDim;
+        const float* Vf = reinterpret_cast<const float*>(ca.v) + (size_t)bh * nkv * kHeadDim;
+        const __amdgpu_buffer_rsrc_t q32 = make_rsrc(Qf, (unsigned)nq * kHeadDim * 4);
+        const __amdgpu_buffer_rsrc_t k32 = make_rsrc(Kf, (unsigned)nkv * kHeadDim * 4);
+        const __amdgpu_buffer_rsrc_t v32 = make_rsrc(Vf, (unsigned)nkv * kHeadDim * 4);
+        struct Tile {
+            Raw8<float> p[8];
+        };
+        const int prow = lane >> 3, pc = lane & 7;
+        auto ld_tile = [&](int j, Tile& x) {  // tile j of the order K(0..), V(0..)
+            const int t = j % TPW;
+            const unsigned base = ((unsigned)(key0 + kTileKV * t + prow) * kHeadDim + 8 * pc) * 4;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) bload8(x.p[i], j < TPW ? k32 : v32, base + i * 8 * kHeadDim * 4, 0);
+        };
+        auto st_tile = [&](int j, const Tile& x) {
+            const unsigned slot = region + (unsigned)(j % TPW) * kTileBytes;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int row = 8 * i + prow;
+                const int pos = j < TPW ? (pc ^ ((row >> 1) & 7)) : (pc ^ (((row >> 1) & 3) << 1));
+                lds_write16(lds, slot + row * 128 + (pos << 4), to_f16(x.p[i]));
+            }
+        };
+        // Q: Q[q_row][32s+8g..+7] rounded to fp16, then scaled as the fp16 path does
+        f16x8 qf[2];
+        {
+            Raw8<float> qr[2];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) bload8(qr[s], q32, (unsigned)(q_row * kHeadDim + 32 * s + 8 * g) * 4, 0);
+            const float sc = kScaleLog2;
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const u32x4 in = __builtin_bit_cast(u32x4, to_f16(qr[s]));
+                u32x4 outv;
+#pragma unroll
+                for (int w = 0; w < 4; ++w)
+                    asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[1,0,0]\n\t"
+                        "v_fma_mixhi_f16 %0, %1, %2, 0 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+                        : "=&v"(outv[w])
+                        : "v"(in[w]), "v"(sc));
+                qf[s] = __builtin_bit_cast(f16x8, outv);
+            }
+        }
+        auto read_k = [&](int t, f16x8(&kf)[4][2]) {
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    kf[kb][s] = lds_read16(lds, region + k_off(kTileKV * t + 16 * kb + i16, 4 * s + g));
+        };
+        const f16x8 ones = f16x8{1, 1, 1, 1, 1, 1, 1, 1};
+        const int qq = (lane & 15) >> 2, pp = lane & 3;
+        const int sw = ((4 * g + qq) >> 1) & 3;
+        unsigned vbase[4];
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+            vbase[db] = region + (unsigned)(4 * g + qq) * 128 + ((2 * (db ^ sw) + (pp >> 1)) << 4) + 8 * (pp & 1);
+        f16x8 p[TPW][2];
+        f32x4 sc[TPW][4];
+        auto pv = [&](int t, bool first) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                for (int db = 0; db < 4; ++db) {
+                    const unsigned off = (unsigned)(t * kTileBytes + 128 * 32 * u);
+                    const f16x8 va = cat8(tr_read(lds, vbase[db] + off), tr_read(lds, vbase[db] + off + 16 * 128));
+                    o[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, p[t][u], (first && u == 0) ? f32x4{} : o[db], 0,
+                                                                   0, 0);
+                }
+                l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ones, p[t][u], (first && u == 0) ? f32x4{} : l_acc, 0,
+                                                               0, 0);
+            }
+        };
+        auto exp_pack = [&](f32x4(&c)[4], f16x8(&pt)[2], float m) {
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) c[kb][e] = __builtin_amdgcn_exp2f(c[kb][e] - m);
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                pt[u] = f16x8{(f16)c[2 * u][0],     (f16)c[2 * u][1],     (f16)c[2 * u][2],     (f16)c[2 * u][3],
+                              (f16)c[2 * u + 1][0], (f16)c[2 * u + 1][1], (f16)c[2 * u + 1][2], (f16)c[2 * u + 1][3]};
+        };
+        auto scores = [&](int t) {
+            f16x8 kf[4][2];
+            read_k(t, kf);
+            f32x4 c[4];
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb) {
+                c[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kb][0], qf[0], f32x4{}, 0, 0, 0);
+                c[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kb][1], qf[1], c[kb], 0, 0, 0);
+            }
+            if (key0 + kTileKV * (t + 1) > nkv) {  // wave-uniform: mask keys past nkv
+#pragma unroll
+                for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (key0 + kTileKV * t + 16 * kb + 4 * g + e >= nkv) c[kb][e] = -INFINITY;
+            }
+            if (t == 0) {
+                const float mx = xquad_max(max16(c));
+                m_run = (mx < kEmptyMax) ? 0.f : mx;
+                exp_pack(c, p[0], m_run);
+            } else {
+#pragma unroll
+                for (int kb = 0; kb < 4; ++kb) sc[t][kb] = c[kb];
+            }
+        };
+        // the pipeline: store tile j, issue tile j + 2, then the scores its store made possible;
+        // V(t) for t >= 2 is stored just before its PV
+#ifndef MHA_F32_NB
+#define MHA_F32_NB 2  // fp32 tiles in flight per wave (A/B hook)
+#endif
+        constexpr int NB = MHA_F32_NB;
+        Tile buf[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) ld_tile(j, buf[j]);
+        constexpr int NJ = TPW + 2;  // tiles stored before the softmax: K(0..TPW-1), V(0), V(1)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            st_tile(j, buf[j % NB]);
+            if (j + NB < 2 * TPW) ld_tile(j + NB, buf[j % NB]);
+            if (j >= 1 && j - 1 < TPW) scores(j - 1);
+        }
+        {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int t = 1; t < TPW; ++t) mx = fmaxf(mx, max16(sc[t]));
+            const float ex = xquad_max(mx) - m_run;
+            if (__builtin_amdgcn_ballot_w64(ex > kRescaleThr) != 0) {
+                const float d = fmaxf(ex, 0.f);
+                const f16 alpha = (f16)__builtin_amdgcn_exp2f(-d);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) p[0][u] *= alpha;
+                m_run += d;
+            }
+        }
+        pv(0, true);
+#pragma unroll
+        for (int t = 1; t < TPW; ++t) exp_pack(sc[t], p[t], m_run);
+#pragma unroll
+        for (int t = 1; t < TPW; ++t) {
+            if (t >= 2) st_tile(TPW + t, buf[(TPW + t) % NB]);
+            pv(t, false);
+        }
     } else {
         // ---- loads, all up front (rows past nkv / nq read as zero through the descriptors) ----
         // DMA piece i = rows 8i..8i+7 of the wave's slice; lane L writes LDS chunk L&7 of row
@@ -475,23 +631,33 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
 #endif
 }
 
-template <typename TOut, int KW, int TPW, int PASSES = 1>
+template <typename TOut, int KW, int TPW, int PASSES = 1, bool F32IN = false>
 hipError_t launch16_t(const FwdArgs& a, int grid, hipStream_t stream) {
     if (a.n_calls > 1)
-        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, true, PASSES>), dim3(grid), dim3(64 * KW), 0, stream,
-                           nullptr, nullptr, nullptr, nullptr, a.total_blocks, 0, 0, 0, a);
+        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, true, PASSES, F32IN>), dim3(grid), dim3(64 * KW), 0,
+                           stream, nullptr, nullptr, nullptr, nullptr, a.total_blocks, 0, 0, 0, a);
     else
-        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, false, PASSES>), dim3(grid), dim3(64 * KW), 0, stream,
-                           a.c[0].q, a.c[0].k, a.c[0].v, a.c[0].o, a.total_blocks, a.c[0].nq, a.c[0].nkv,
+        hipLaunchKernelGGL((mha_hd64_direct16_kernel<TOut, KW, TPW, false, PASSES, F32IN>), dim3(grid), dim3(64 * KW), 0,
+                           stream, a.c[0].q, a.c[0].k, a.c[0].v, a.c[0].o, a.total_blocks, a.c[0].nq, a.c[0].nkv,
                            a.c[0].qtiles, a);
     return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch_direct16(const FwdArgs& a, int grid, int tiles_per_wave, bool out_f32, hipStream_t stream) {
+hipError_t launch_direct16(const FwdArgs& a, int grid, int tiles_per_wave, bool out_f32, hipStream_t stream,
+                           bool in_f32) {
     // tiles_per_wave counts 64-key tiles per wave of the 8-wave form (1: nkv <= 512, 2: <= 1024);
     // 4 waves take twice as many
+    if (in_f32) {  // fp32 Q/K/V converted in the kernel (one-pass forms only: nkv <= 1024)
+        switch (tiles_per_wave * 2 + (out_f32 ? 1 : 0)) {
+            case 2: return launch16_t<f16, 4, 2, 1, true>(a, grid, stream);
+            case 3: return launch16_t<float, 4, 2, 1, true>(a, grid, stream);
+            case 4: return launch16_t<f16, 4, 4, 1, true>(a, grid, stream);
+            case 5: return launch16_t<float, 4, 4, 1, true>(a, grid, stream);
+            default: return hipErrorInvalidValue;
+        }
+    }
     if (tiles_per_wave > 2)  // nkv in (1024, 2048]: 4 waves x two passes of 4 tiles
         return out_f32 ? launch16_t<float, 4, 4, 2>(a, grid, stream) : launch16_t<f16, 4, 4, 2>(a, grid, stream);
     switch (tiles_per_wave * 2 + (out_f32 ? 1 : 0)) {

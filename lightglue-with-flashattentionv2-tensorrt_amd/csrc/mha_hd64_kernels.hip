@@ -1212,7 +1212,22 @@ bool f32_convert_enabled() {
     }();
     return on;
 }
+// fp32 inputs rounded inside the 16-row kernel (one launch) where its one-pass forms apply
+// (MHA_HD64_F32_INKERNEL=0 or set_f32_inkernel(0): the convert launch + fp16 kernel instead)
+std::atomic<int> g_f32_inkernel{-1};
+bool f32_inkernel_enabled() {
+    int v = g_f32_inkernel.load();
+    if (v < 0) {
+        const char* e = std::getenv("MHA_HD64_F32_INKERNEL");
+        int expect = -1;
+        g_f32_inkernel.compare_exchange_strong(expect, (e && e[0] == '0') ? 0 : 1);
+        v = g_f32_inkernel.load();
+    }
+    return v == 1;
+}
 }  // namespace
+
+void set_f32_inkernel(int enable) { g_f32_inkernel.store(enable ? 1 : 0); }
 
 static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutType out, void* workspace,
                                      size_t ws_bytes, hipStream_t stream, int force_q_waves, int force_kv_waves,
@@ -1260,12 +1275,20 @@ static hipError_t launch_f32_via_f16(const Call* calls, int n, OutType out, void
 static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutType out, void* workspace,
                                      size_t ws_bytes, hipStream_t stream, int force_q_waves, int force_kv_waves,
                                      int force_splits, int phase_mask) {
+    bool in32_direct = false;  // fp32 inputs into the 16-row kernel's one-pass forms
+    GroupPlan p{};
     if (in == InType::F32 && force_q_waves == 0 && force_kv_waves == 0 && force_splits == 0) {
-        const hipError_t e = launch_f32_via_f16(calls, n, out, workspace, ws_bytes, stream, phase_mask);
-        if (e != hipErrorNotSupported) return e;
+        if (f32_inkernel_enabled() && f32_convert_enabled()) {
+            const GroupPlan p16 = plan_group(calls, n, 0, 0, 0, 0, InType::F16);
+            in32_direct = p16.direct_tiles > 0 && p16.direct_tiles <= 2 && p16.rows_per_wave == 16;
+            if (in32_direct) p = p16;
+        }
+        if (!in32_direct) {
+            const hipError_t e = launch_f32_via_f16(calls, n, out, workspace, ws_bytes, stream, phase_mask);
+            if (e != hipErrorNotSupported) return e;
+        }
     }
-    const GroupPlan p =
-        plan_group(calls, n, workspace ? ws_bytes : 0, force_q_waves, force_kv_waves, force_splits, in);
+    if (!in32_direct) p = plan_group(calls, n, workspace ? ws_bytes : 0, force_q_waves, force_kv_waves, force_splits, in);
     FwdArgs a{};
     CombineArgs cb{};
     a.stamps = g_stamps;
@@ -1311,7 +1334,7 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
     if (p.direct_tiles > 0) {  // single-pass kernel: no split, no workspace
         g_last_combine = 0;
         if (!(phase_mask & 1)) return hipSuccess;
-        return p.rows_per_wave == 16 ? launch_direct16(a, blocks, p.direct_tiles, out == OutType::F32, stream)
+        return p.rows_per_wave == 16 ? launch_direct16(a, blocks, p.direct_tiles, out == OutType::F32, stream, in32_direct)
                                      : launch_direct(a, blocks, p.direct_tiles, out == OutType::F32, stream);
     }
     // Split calls combine inside the main launch when a ticket array is available (phase_mask 3,

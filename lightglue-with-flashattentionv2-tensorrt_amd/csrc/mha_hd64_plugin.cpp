@@ -355,9 +355,10 @@ const char* mha_hd64_last_error(void) { return g_last_error.c_str(); }
 void mha_hd64_set_abort_on_error(int32_t enable) { g_abort_on_error = enable != 0; }
 int32_t mha_hd64_set_concurrency_hint(int32_t streams) { return mha_hd64::set_concurrency_hint(streams); }
 const char* mha_hd64_build_info(void) {
-    return "mha_hd64: gfx950 (CDNA4) HIP kernels, v_mfma_f32_32x32x16_f16 + ds_read_b64_tr_b16; "
-           "variants fp16->fp16, fp16->fp32, fp32->fp32; single-pass kernel (32 rows x all keys per workgroup, K/V by LDS-DMA) "
-           "for launches of <= 256 blocks with nkv <= 1024; LDS-ring kernel with workgroups (q,kv waves) 4x1 2x2 1x2 4x2 2x4 1x4 1x8, "
+    return "mha_hd64: gfx950 (CDNA4) HIP kernels, v_mfma_f32_32x32x16_f16 / 16x16x32_f16 + ds_read_b64_tr_b16; "
+           "variants fp16->fp16, fp16->fp32, fp32->fp32; single-pass kernels (16 or 32 rows x all keys per workgroup, "
+           "K/V by LDS-DMA, L2 prefetch of late rows; fp32 inputs rounded in the 16-row kernel) "
+           "for launches of <= 256 blocks with nkv <= 2048; LDS-ring kernel with workgroups (q,kv waves) 4x1 2x2 1x2 4x2 2x4 1x4 1x8, "
            "2x2 with 64-row waves; software-pipelined QK(t+1)|softmax(t); split-KV combine (in-launch or kernel)";
 }
 
@@ -401,6 +402,9 @@ void mha_hd64_set_stamp_buffer(void* p) { mha_hd64::set_stamp_buffer(p); }
 
 // Test/bench hook: 1 = split calls combine inside the main launch (default), 0 = combine kernel.
 void mha_hd64_set_fused_combine(int32_t enable) { mha_hd64::set_fused_combine(enable); }
+// Test/bench hook: fp32 Q/K/V rounded to fp16 inside the 16-row kernel (1, default where it
+// applies) or by a separate convert launch before the fp16 kernel (0); results are bitwise equal.
+void mha_hd64_set_f32_inkernel(int32_t enable) { mha_hd64::set_f32_inkernel(enable); }
 // Test hook: 0 = the calling thread's last launch had no split, 1 = in-launch combine, 2 = combine kernel.
 int32_t mha_hd64_last_combine_form(void) { return mha_hd64::last_combine_form(); }
 

@@ -142,6 +142,7 @@ HOOKS = {
     "mha_hd64_plan": ([_I, _I, _I, _I, _S, ctypes.POINTER(ctypes.c_int32)], _S),
     "mha_hd64_set_stamp_buffer": ([_P], None),
     "mha_hd64_set_fused_combine": ([_I], None),
+    "mha_hd64_set_f32_inkernel": ([_I], None),
     "mha_hd64_last_combine_form": ([], _I),
 }
 

@@ -6,6 +6,8 @@ fp16-rounded inputs (o_ref16), the Float path on the raw fp32 inputs (o_ref32; t
 kernel rounds them to fp16 on load exactly like the reference's convert kernel).
 Observed errors are ~1e-3 (fp16 output rounding + fp16 P); TOL_* below are the contract.
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -160,6 +162,51 @@ def test_forced_plans_f32_input(wg, dev, oracle_mod):
     assert st == 0, _lib.last_error()
     torch.cuda.synchronize()
     assert _maxdiff(o.cpu().numpy(), ref) <= TOL
+
+
+F32_SHAPES = [(1, 1), (33, 65), (100, 100), (300, 129), (512, 512), (777, 1000), (1024, 768), (1024, 1024),
+              (64, 2048), (16, 4500)]
+
+
+@pytest.mark.parametrize("nq,nkv", F32_SHAPES)
+@pytest.mark.parametrize("batch,heads", [(1, 4), (2, 3)])
+def test_float_boundary_in_kernel_equals_convert_launch(nq, nkv, batch, heads, dev, oracle_mod):
+    """fp32 Q/K/V rounded to fp16 inside the 16-row kernel (one launch) vs the convert launch +
+    fp16 kernel: both round every input RNE and then run the same arithmetic, so the outputs are
+    bitwise equal. The in-kernel form leaves the workspace untouched (no converted copy is
+    written: one launch), the convert form fills it; shapes past the one-pass forms (nkv > 1024,
+    more than 256 blocks) take the convert form either way."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    qn, kn, vn = synth.qkv(77 + nq + nkv, nq, nkv, batch=batch, heads=heads)
+    q, k, v = (_t(x, dev, torch.float32) for x in (qn, kn, vn))
+    plan = (ctypes.c_int32 * 4)()
+    lib.mha_hd64_plan(batch, heads, nq, nkv, 64 << 20, plan)
+    one_pass16 = plan[0] == 22 and nkv <= 1024
+    outs, touched = [], []
+    for inkernel in (1, 0):
+        lib.mha_hd64_set_f32_inkernel(inkernel)
+        try:
+            ws = torch.full((64 << 20,), 0x5A, dtype=torch.uint8, device=dev)
+            o = torch.full(q.shape, float("nan"), dtype=torch.float32, device=dev)
+            st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), batch, heads,
+                                            nq, nkv, 1, 1, 0, 0, 0, ws.data_ptr(), ws.numel(),
+                                            torch.cuda.current_stream().cuda_stream, 3)
+            assert st == 0, _lib.last_error()
+            torch.cuda.synchronize()
+        finally:
+            lib.mha_hd64_set_f32_inkernel(1)
+        outs.append(o)
+        touched.append(bool((ws[: 1 << 20] != 0x5A).any()))
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
+    if one_pass16:
+        assert not touched[0], "in-kernel form wrote the workspace (a convert launch ran)"
+        assert touched[1]
+    rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 24)), nq - 1])
+    ref = oracle_mod.attention_c(np.ascontiguousarray(qn[:, :, rows]), kn, vn)
+    assert _maxdiff(outs[0].cpu().numpy()[:, :, rows], ref) <= TOL
 
 
 def test_rescale_branch_forced(dev, oracle_mod):

@@ -79,6 +79,75 @@ __global__ __launch_bounds__(NT) void dma_kernel(const u32x4* K, const u32x4* V,
     O[(size_t)blockIdx.x * NT + threadIdx.x] = *(const u32x4*)(lds + threadIdx.x * 16);
 }
 
+// fp32 K/V (256-B rows, the Float boundary's inputs) by LDS-DMA, 16 B per lane per instruction:
+// twice the pieces of dma_kernel for the same keys.
+template <int KPW, int NT = 256>
+__global__ __launch_bounds__(NT) void dma32_kernel(const u32x4* K, const u32x4* V, u32x4* O, int span) {
+    __shared__ __attribute__((aligned(16))) char lds[4 * 32768];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int xcd = blockIdx.x & 7, idx = blockIdx.x >> 3;
+    const int per_xcd = gridDim.x >> 3;
+    const int head = xcd >> 1;
+    const int local = (xcd & 1) * per_xcd + idx;
+    const int split = local % (1024 / span);
+    const int key0 = split * span + wave * KPW;
+    const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc((void*)(K + (size_t)head * 1024 * 16), (short)0, 1 << 18, 0x00020000);
+    const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc((void*)(V + (size_t)head * 1024 * 16), (short)0, 1 << 18, 0x00020000);
+    constexpr int N = KPW / 4;  // 1 KiB pieces per tensor
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (__attribute__((address_space(3))) void*)(lds + wave * 32768 + (i & 31) * 1024), 16,
+                                                 (unsigned)(key0 * 256 + lane * 16), i * 1024, 0, 0);
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(vr, (__attribute__((address_space(3))) void*)(lds + wave * 32768 + ((i + N) & 31) * 1024), 16,
+                                                 (unsigned)(key0 * 256 + lane * 16), i * 1024, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    O[(size_t)blockIdx.x * NT + threadIdx.x] = *(const u32x4*)(lds + threadIdx.x * 16);
+}
+
+// fp32 K/V through VGPRs, converted to fp16 and written to LDS (what a one-launch Float boundary
+// would do per workgroup): 16 rows x 1024 keys per workgroup, 4 waves x 256 keys, 8 chunk
+// loads in flight per batch.
+template <int KPW, int NT = 256>
+__global__ __launch_bounds__(NT) void cvt32_kernel(const u32x4* K, const u32x4* V, u32x4* O, int span) {
+    __shared__ __attribute__((aligned(16))) char lds[4 * 16384];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int xcd = blockIdx.x & 7, idx = blockIdx.x >> 3;
+    const int per_xcd = gridDim.x >> 3;
+    const int head = xcd >> 1;
+    const int local = (xcd & 1) * per_xcd + idx;
+    const int split = local % (1024 / span);
+    const int key0 = split * span + wave * KPW;
+    constexpr int N = KPW / 8;  // 8-row pieces per tensor (one 32-B, 8-float chunk per lane each)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const u32x4* base = (t == 0 ? K : V) + (size_t)head * 1024 * 16 + (size_t)key0 * 16;
+#pragma unroll 4
+        for (int b = 0; b < N / 16; ++b) {
+            u32x4 r[32];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                r[2 * i] = base[(b * 16 + i) * 128 + 2 * lane];
+                r[2 * i + 1] = base[(b * 16 + i) * 128 + 2 * lane + 1];
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float* f = reinterpret_cast<const float*>(&r[2 * i]);
+                typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+                h8 h = {(_Float16)f[0], (_Float16)f[1], (_Float16)f[2], (_Float16)f[3],
+                        (_Float16)f[4], (_Float16)f[5], (_Float16)f[6], (_Float16)f[7]};
+                *reinterpret_cast<__attribute__((address_space(3))) h8*>(
+                    (__attribute__((address_space(3))) char*)lds + wave * 16384 + ((b * 16 + i) & 15) * 1024 + lane * 16) = h;
+            }
+            asm volatile("" ::: "memory");  // the overwritten stores stay (no dead-store elimination)
+        }
+    }
+    __syncthreads();
+    O[(size_t)blockIdx.x * NT + threadIdx.x] = *(const u32x4*)(lds + threadIdx.x * 16);
+}
+
 __global__ void empty_kernel() {}
 
 template <typename F>
@@ -140,6 +209,10 @@ int main() {
            time_graph([&] { dma_kernel<256, 256><<<128, 256, 0, s>>>(K, V, O, 1024); }, s, C));
     printf(", \"dma_nosplit16_256x256_kpw256_us\": %.3f",
            time_graph([&] { dma_kernel<256, 256><<<256, 256, 0, s>>>(K, V, O, 1024); }, s, C));
+    printf(", \"dma32_nosplit16_256x256_kpw256_us\": %.3f",
+           time_graph([&] { dma32_kernel<256><<<256, 256, 0, s>>>(K, V, O, 1024); }, s, C));
+    printf(", \"cvt32_nosplit16_256x256_kpw256_us\": %.3f",
+           time_graph([&] { cvt32_kernel<256><<<256, 256, 0, s>>>(K, V, O, 1024); }, s, C));
     printf("}\n");
     return 0;
 }
