@@ -328,7 +328,7 @@ def load_traffic(tag):
 def variants(torch, lightglue_amd, device, stream, q, k, v, flops):
     """BASELINE configs[2] and the plugin's Float boundary at the metric shape: fp16 in -> fp32 out
     (the reference's fp16in_fp32out kernel) and fp32 Q/K/V -> fp32 O (a TensorRT fp32 engine's
-    call: convert + fp16 kernel). Per-call time from a graph of 200 back-to-back calls, and the
+    call: one launch, the inputs rounded to fp16 inside the 16-row kernel). Per-call time from a graph of 200 back-to-back calls, and the
     max-abs error against a PyTorch fp32 attention of the same (fp16-valued) inputs on the GPU
     (lightglue_pytorch_no_plugin/lightglue.py:82-84; north_star tolerance 1e-2)."""
     qf, kf, vf = (t.float() for t in (q, k, v))
