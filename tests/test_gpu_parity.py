@@ -209,6 +209,27 @@ def test_float_boundary_in_kernel_equals_convert_launch(nq, nkv, batch, heads, d
     assert _maxdiff(outs[0].cpu().numpy()[:, :, rows], ref) <= TOL
 
 
+@pytest.mark.parametrize("shapes", [[(1024, 1024)], [(512, 512), (300, 257)], [(33, 65), (777, 1000), (64, 128)]])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.float16])
+def test_float_inputs_equal_fp16_inputs_rounded_on_host(shapes, out_dtype, dev):
+    """The in-kernel rounding of fp32 Q/K/V (single and grouped launches, fp32 or fp16 output)
+    is the host's RNE rounding: the fp32-input launch equals the fp16-input launch on
+    round_f16(inputs) bit for bit (same plan, same kernel, same arithmetic after the loads)."""
+    from lightglue_amd import mha_hd64_grouped, synth
+
+    calls32, calls16 = [], []
+    for i, (nq, nkv) in enumerate(shapes):
+        qn, kn, vn = synth.qkv(500 + 13 * i + nq, nq, nkv)
+        calls32.append(tuple(_t(x, dev, torch.float32) for x in (qn, kn, vn)))
+        calls16.append(tuple(_t(synth.round_f16(x), dev, torch.float16) for x in (qn, kn, vn)))
+    o32 = mha_hd64_grouped(calls32, out_dtype=out_dtype)
+    o16 = mha_hd64_grouped(calls16, out_dtype=out_dtype)
+    torch.cuda.synchronize()
+    for a, b in zip(o32, o16):
+        assert torch.isfinite(a.float()).all()
+        assert torch.equal(a, b)
+
+
 def test_rescale_branch_forced(dev, oracle_mod):
     """Rule 26 (cdna_hip_programming.md §5.4): force the lazy-rescale branch at a chosen tile.
 
