@@ -104,7 +104,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
                                                                         int qtiles0, FwdArgs a) {
     static_assert(TPW >= 2 && TPW <= 4 && (KW == 4 || KW == 8), "waves x tiles per wave");
     static_assert(PASSES == 1 || (PASSES == 2 && TPW == 4 && KW == 4), "two passes: 4 waves x 2 x 4 tiles");
-    static_assert(!F32IN || (PASSES == 1 && KW == 4), "fp32 inputs: the one-pass 4-wave forms");
+    static_assert(!F32IN || KW == 4, "fp32 inputs: the 4-wave forms");
     constexpr int BLOCK_M = 16;                     // query rows per workgroup
     constexpr int WAVE_KEYS = kTileKV * TPW * PASSES;
     constexpr int OROW = 68;                        // epilogue fp32 row pitch
@@ -189,18 +189,22 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
             Raw8<float> p[8];
         };
         const int prow = lane >> 3, pc = lane & 7;
-        auto ld_tile = [&](int j, Tile& x) {  // tile j of the order K(0..), V(0..)
-            const int t = j % TPW;
+        // item j of the order K(0..TPW-1), V(0..TPW-1) of pass 0, then the same for pass 1:
+        // tile TPW·pass + (j % TPW) of K (first half of the pass) or V, into slot j % TPW
+        constexpr int NI = 2 * TPW * PASSES;
+        auto ld_tile = [&](int j, Tile& x) {
+            const int r = j % (2 * TPW), t = (j / (2 * TPW)) * TPW + r % TPW;
             const unsigned base = ((unsigned)(key0 + kTileKV * t + prow) * kHeadDim + 8 * pc) * 4;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) bload8(x.p[i], j < TPW ? k32 : v32, base + i * 8 * kHeadDim * 4, 0);
+            for (int i = 0; i < 8; ++i) bload8(x.p[i], r < TPW ? k32 : v32, base + i * 8 * kHeadDim * 4, 0);
         };
         auto st_tile = [&](int j, const Tile& x) {
-            const unsigned slot = region + (unsigned)(j % TPW) * kTileBytes;
+            const int r = j % (2 * TPW);
+            const unsigned slot = region + (unsigned)(r % TPW) * kTileBytes;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int row = 8 * i + prow;
-                const int pos = j < TPW ? (pc ^ ((row >> 1) & 7)) : (pc ^ (((row >> 1) & 3) << 1));
+                const int pos = r < TPW ? (pc ^ ((row >> 1) & 7)) : (pc ^ (((row >> 1) & 3) << 1));
                 lds_write16(lds, slot + row * 128 + (pos << 4), to_f16(x.p[i]));
             }
         };
@@ -264,7 +268,8 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
                 pt[u] = f16x8{(f16)c[2 * u][0],     (f16)c[2 * u][1],     (f16)c[2 * u][2],     (f16)c[2 * u][3],
                               (f16)c[2 * u + 1][0], (f16)c[2 * u + 1][1], (f16)c[2 * u + 1][2], (f16)c[2 * u + 1][3]};
         };
-        auto scores = [&](int t) {
+        auto scores = [&](int tile) {  // tile TPW·pass + t, in slot t
+            const int t = tile % TPW;
             f16x8 kf[4][2];
             read_k(t, kf);
             f32x4 c[4];
@@ -273,14 +278,14 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
                 c[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kb][0], qf[0], f32x4{}, 0, 0, 0);
                 c[kb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kb][1], qf[1], c[kb], 0, 0, 0);
             }
-            if (key0 + kTileKV * (t + 1) > nkv) {  // wave-uniform: mask keys past nkv
+            if (key0 + kTileKV * (tile + 1) > nkv) {  // wave-uniform: mask keys past nkv
 #pragma unroll
                 for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
-                        if (key0 + kTileKV * t + 16 * kb + 4 * g + e >= nkv) c[kb][e] = -INFINITY;
+                        if (key0 + kTileKV * tile + 16 * kb + 4 * g + e >= nkv) c[kb][e] = -INFINITY;
             }
-            if (t == 0) {
+            if (tile == 0) {
                 const float mx = xquad_max(max16(c));
                 m_run = (mx < kEmptyMax) ? 0.f : mx;
                 exp_pack(c, p[0], m_run);
@@ -289,8 +294,9 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
                 for (int kb = 0; kb < 4; ++kb) sc[t][kb] = c[kb];
             }
         };
-        // the pipeline: store tile j, issue tile j + 2, then the scores its store made possible;
-        // V(t) for t >= 2 is stored just before its PV
+        // the pipeline: store item j, issue item j + NB, then the scores its store made possible;
+        // V(t) for t >= 2 is stored just before its PV (its slot's K was read by then); pass 1's
+        // K(t) goes into slot t once pass 0's PV(t) has read V(t)
 #ifndef MHA_F32_NB
 #define MHA_F32_NB 2  // fp32 tiles in flight per wave (A/B hook)
 #endif
@@ -298,33 +304,48 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         Tile buf[NB];
 #pragma unroll
         for (int j = 0; j < NB; ++j) ld_tile(j, buf[j]);
-        constexpr int NJ = TPW + 2;  // tiles stored before the softmax: K(0..TPW-1), V(0), V(1)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
+        auto store = [&](int j) {  // item j into its slot, then the load NB items ahead
             st_tile(j, buf[j % NB]);
-            if (j + NB < 2 * TPW) ld_tile(j + NB, buf[j % NB]);
-            if (j >= 1 && j - 1 < TPW) scores(j - 1);
-        }
-        {
-            float mx = -INFINITY;
+            if (j + NB < NI) ld_tile(j + NB, buf[j % NB]);
+        };
 #pragma unroll
-            for (int t = 1; t < TPW; ++t) mx = fmaxf(mx, max16(sc[t]));
-            const float ex = xquad_max(mx) - m_run;
-            if (__builtin_amdgcn_ballot_w64(ex > kRescaleThr) != 0) {
-                const float d = fmaxf(ex, 0.f);
-                const f16 alpha = (f16)__builtin_amdgcn_exp2f(-d);
+        for (int ps = 0; ps < PASSES; ++ps) {
+            const int b = 2 * TPW * ps, t0 = TPW * ps;
 #pragma unroll
-                for (int u = 0; u < 2; ++u) p[0][u] *= alpha;
-                m_run += d;
+            for (int j = 0; j < TPW + 2; ++j) {  // K(0..TPW-1), V(0), V(1) of the pass
+                store(b + j);
+                if (j >= 1 && j - 1 < TPW) scores(t0 + j - 1);
             }
-        }
-        pv(0, true);
+            // ONE rescale decision per pass (wave-uniform, rare): pass 0 against the first
+            // tile's max (its P rescaled), later passes against the running max (O and l rescaled)
+            {
+                float mx = -INFINITY;
 #pragma unroll
-        for (int t = 1; t < TPW; ++t) exp_pack(sc[t], p[t], m_run);
+                for (int t = (ps == 0 ? 1 : 0); t < TPW; ++t) mx = fmaxf(mx, max16(sc[t]));
+                const float ex = xquad_max(mx) - m_run;
+                if (__builtin_amdgcn_ballot_w64(ex > kRescaleThr) != 0) {
+                    const float d = fmaxf(ex, 0.f);
+                    if (ps == 0) {
+                        const f16 alpha = (f16)__builtin_amdgcn_exp2f(-d);
 #pragma unroll
-        for (int t = 1; t < TPW; ++t) {
-            if (t >= 2) st_tile(TPW + t, buf[(TPW + t) % NB]);
-            pv(t, false);
+                        for (int u = 0; u < 2; ++u) p[0][u] *= alpha;
+                    } else {
+                        const float alpha = __builtin_amdgcn_exp2f(-d);
+#pragma unroll
+                        for (int db = 0; db < 4; ++db) o[db] *= alpha;
+                        l_acc *= alpha;
+                    }
+                    m_run += d;
+                }
+            }
+            if (ps == 0) pv(0, true);
+#pragma unroll
+            for (int t = (ps == 0 ? 1 : 0); t < TPW; ++t) exp_pack(sc[t], p[t], m_run);
+#pragma unroll
+            for (int t = (ps == 0 ? 1 : 0); t < TPW; ++t) {
+                if (t >= 2) store(b + TPW + t);
+                pv(t, false);
+            }
         }
     } else {
         // ---- loads, all up front (rows past nkv / nq read as zero through the descriptors) ----
@@ -649,7 +670,7 @@ hipError_t launch_direct16(const FwdArgs& a, int grid, int tiles_per_wave, bool 
                            bool in_f32) {
     // tiles_per_wave counts 64-key tiles per wave of the 8-wave form (1: nkv <= 512, 2: <= 1024);
     // 4 waves take twice as many
-    if (in_f32) {  // fp32 Q/K/V converted in the kernel (one-pass forms only: nkv <= 1024)
+    if (in_f32) {  // fp32 Q/K/V rounded in the kernel: the one-pass forms (the planner's choice)
         switch (tiles_per_wave * 2 + (out_f32 ? 1 : 0)) {
             case 2: return launch16_t<f16, 4, 2, 1, true>(a, grid, stream);
             case 3: return launch16_t<float, 4, 2, 1, true>(a, grid, stream);

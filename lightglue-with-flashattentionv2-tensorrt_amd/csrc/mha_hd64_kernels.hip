@@ -1280,6 +1280,9 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
     if (in == InType::F32 && force_q_waves == 0 && force_kv_waves == 0 && force_splits == 0) {
         if (f32_inkernel_enabled() && f32_convert_enabled()) {
             const GroupPlan p16 = plan_group(calls, n, 0, 0, 0, 0, InType::F16);
+            // one-pass forms only (nkv <= 1024): the two-pass form rounding fp32 in the kernel
+            // measured slower than convert + fp16 kernel (1x4x1024x2048 11.32 vs 10.75 us,
+            // 512x1536 9.78 vs 9.24; profiles/r02/float_inkernel.jsonl)
             in32_direct = p16.direct_tiles > 0 && p16.direct_tiles <= 2 && p16.rows_per_wave == 16;
             if (in32_direct) p = p16;
         }

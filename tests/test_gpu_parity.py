@@ -165,7 +165,7 @@ def test_forced_plans_f32_input(wg, dev, oracle_mod):
 
 
 F32_SHAPES = [(1, 1), (33, 65), (100, 100), (300, 129), (512, 512), (777, 1000), (1024, 768), (1024, 1024),
-              (64, 2048), (16, 4500)]
+              (64, 2048), (1024, 2048), (700, 1500), (16, 4500)]
 
 
 @pytest.mark.parametrize("nq,nkv", F32_SHAPES)
@@ -174,8 +174,8 @@ def test_float_boundary_in_kernel_equals_convert_launch(nq, nkv, batch, heads, d
     """fp32 Q/K/V rounded to fp16 inside the 16-row kernel (one launch) vs the convert launch +
     fp16 kernel: both round every input RNE and then run the same arithmetic, so the outputs are
     bitwise equal. The in-kernel form leaves the workspace untouched (no converted copy is
-    written: one launch), the convert form fills it; shapes past the one-pass forms (nkv > 1024,
-    more than 256 blocks) take the convert form either way."""
+    written: one launch), the convert form fills it; other launches (nkv > 1024, more than 256
+    blocks) take the convert form or the ring kernel either way."""
     from lightglue_amd import _lib, synth
 
     lib = _lib.load()
@@ -183,7 +183,7 @@ def test_float_boundary_in_kernel_equals_convert_launch(nq, nkv, batch, heads, d
     q, k, v = (_t(x, dev, torch.float32) for x in (qn, kn, vn))
     plan = (ctypes.c_int32 * 4)()
     lib.mha_hd64_plan(batch, heads, nq, nkv, 64 << 20, plan)
-    one_pass16 = plan[0] == 22 and nkv <= 1024
+    in_kernel = plan[0] == 22 and nkv <= 1024  # the 16-row kernel's one-pass forms take fp32 directly
     outs, touched = [], []
     for inkernel in (1, 0):
         lib.mha_hd64_set_f32_inkernel(inkernel)
@@ -201,7 +201,7 @@ def test_float_boundary_in_kernel_equals_convert_launch(nq, nkv, batch, heads, d
         touched.append(bool((ws[: 1 << 20] != 0x5A).any()))
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1])
-    if one_pass16:
+    if in_kernel:
         assert not touched[0], "in-kernel form wrote the workspace (a convert launch ran)"
         assert touched[1]
     rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 24)), nq - 1])
@@ -209,7 +209,8 @@ def test_float_boundary_in_kernel_equals_convert_launch(nq, nkv, batch, heads, d
     assert _maxdiff(outs[0].cpu().numpy()[:, :, rows], ref) <= TOL
 
 
-@pytest.mark.parametrize("shapes", [[(1024, 1024)], [(512, 512), (300, 257)], [(33, 65), (777, 1000), (64, 128)]])
+@pytest.mark.parametrize("shapes", [[(1024, 1024)], [(512, 512), (300, 257)], [(33, 65), (777, 1000), (64, 128)],
+                                    [(1024, 2048)], [(200, 1500), (64, 2048)]])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.float16])
 def test_float_inputs_equal_fp16_inputs_rounded_on_host(shapes, out_dtype, dev):
     """The in-kernel rounding of fp32 Q/K/V (single and grouped launches, fp32 or fp16 output)
