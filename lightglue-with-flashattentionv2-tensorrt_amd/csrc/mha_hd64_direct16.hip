@@ -298,9 +298,11 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         // V(t) for t >= 2 is stored just before its PV (its slot's K was read by then); pass 1's
         // K(t) goes into slot t once pass 0's PV(t) has read V(t)
 #ifndef MHA_F32_NB
-#define MHA_F32_NB 2  // fp32 tiles in flight per wave (A/B hook)
+#define MHA_F32_NB 0  // fp32 tiles in flight per wave (A/B hook; 0 = per form)
 #endif
-        constexpr int NB = MHA_F32_NB;
+        // 3 for the 2-tile form (1x4x512^2 5.00 vs 5.10 us), 2 for the 4-tile form (the third
+        // buffer lands in AGPRs: 1024^2 7.45-7.51 vs 7.11; tools/f32_probe.py over MHA_F32_NB builds)
+        constexpr int NB = MHA_F32_NB > 0 ? MHA_F32_NB : (TPW == 2 ? 3 : 2);
         Tile buf[NB];
 #pragma unroll
         for (int j = 0; j < NB; ++j) ld_tile(j, buf[j]);
