@@ -157,6 +157,19 @@ def timed_replays(torch, replay, stream, barrier, reduce_max, replays):
     return reduce_max(med), reduce_max(wall)
 
 
+def claim_stdout(ws):
+    """Rank 0's ONE JSON line is the only thing a bench process writes to stdout. With several
+    ranks, file descriptor 1 is pointed at stderr (the gloo library prints its connection messages
+    to the C-level stdout of every rank) and the returned stream, a private copy of the original
+    stdout, carries the line. One rank: sys.stdout, untouched."""
+    if ws <= 1:
+        return sys.stdout
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 def make_collectives(torch, dist, device=None):
     """Barrier and max-reduce over ranks on a CPU (gloo) group: the replicas exchange nothing on
     the data path, so no RCCL communicator is created (north_star: no collectives needed)."""
@@ -673,6 +686,7 @@ def main():
     if visible_devices() <= local and not share:
         print(f"bench.py: rank {rank} needs GPU {local}, {visible_devices()} visible", file=sys.stderr, flush=True)
         sys.exit(2)
+    result_out = claim_stdout(ws)
     dist = None
     device = torch.device("cuda", local % max(1, visible_devices()) if share else local)
     torch.cuda.set_device(device)
@@ -925,7 +939,7 @@ def main():
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and not args.quick:  # CPU baseline: N=1 only
         result["cpu_baseline"] = cpu_baseline(args.cpu_seconds, nq, nkv)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=result_out, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

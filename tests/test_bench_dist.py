@@ -2,11 +2,16 @@
 rehearsed with world_size-2 gloo on CPU."""
 import os
 import socket
+import subprocess
+import sys
 
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -142,3 +147,19 @@ def test_bench_refuses_world_size_mismatch():
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2
     assert "--gpus 1 but WORLD_SIZE=2" in r.stderr
+
+
+def test_claim_stdout_keeps_only_the_json_line():
+    """With several ranks, C-level writes to fd 1 (gloo's connection messages) land on stderr and
+    only the line written to the claimed stream reaches stdout."""
+    code = (
+        "import os, sys; sys.path.insert(0, %r); import bench\n"
+        "out = bench.claim_stdout(4)\n"
+        "os.write(1, b'[Gloo] Rank 0 is connected to 3 peer ranks\\n')\n"
+        "print('noise from python')\n"
+        "print('{\"metric\": 1}', file=out, flush=True)\n"
+    ) % REPO
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == '{"metric": 1}'
+    assert "Gloo" in r.stderr and "noise from python" in r.stderr
