@@ -110,11 +110,12 @@ def timed_region(run_steps, barrier, sync, reduce_max):
     return reduce_max(dt)
 
 
-def timed_replays(torch, replay, stream, barrier, reduce_max, replays):
+def timed_replays(torch, replay, stream, barrier, reduce_max, replays, local=None):
     """The headline's timed region: barrier + synchronize, then `replays` replays of the K-step
     graph back to back on the launch stream with a HIP event pair around each (events on the stream
     the kernels run on), synchronize + barrier. Returns (max over ranks of the median replay time,
-    max over ranks of the host wall time per replay), in seconds.
+    max over ranks of the host wall time per replay), in seconds; `local` (a dict), if given,
+    receives this rank's own median under "median_s".
 
     The event pair times exactly the K steps on the GPU. A sleep kernel queued ahead of the replays
     holds the stream while the host submits them (sized from an untimed rehearsal of the host's
@@ -154,6 +155,8 @@ def timed_replays(torch, replay, stream, barrier, reduce_max, replays):
     wall = (time.perf_counter() - t0) / replays
     barrier()
     med = statistics.median(s.elapsed_time(e) for s, e in zip(starts, ends)) * 1e-3
+    if local is not None:
+        local["median_s"] = med
     return reduce_max(med), reduce_max(wall)
 
 
@@ -724,11 +727,12 @@ def main():
     stream.synchronize()
 
     replays = args.replays if args.replays > 0 else max(10, min(250, -(-5000 // args.steps)))
-    elapsed, wall = timed_replays(torch, graph.replay, stream, barrier, reduce_max, replays)
+    mine = {}
+    elapsed, wall = timed_replays(torch, graph.replay, stream, barrier, reduce_max, replays, local=mine)
     total_calls = args.steps * ws
     value = total_calls / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
-    rank_values = gather(dist, round(args.steps / elapsed, 1))
+    rank_values = gather(dist, round(args.steps / mine["median_s"], 1))  # each rank's own rate
     # Each replay of a K-step graph pays a fixed ~9 us of graph launch + ~4.8 us for its event pair
     # on the GPU (tools/timing_probe.py, profiles/r02/timing_probe.txt); at the driver's K = 20
     # that is ~10 % of the step time. The same calls in 2000-step graphs, for comparison:
