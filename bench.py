@@ -68,23 +68,44 @@ def _free_port():
 
 
 def visible_devices():
-    """GPU count without initialising the HIP runtime in this process (torch.cuda.device_count()
-    does not, on this image), so the launcher may still start its ranks afterwards."""
+    """GPU count inside a rank process (which initialises HIP itself right after)."""
     import torch
 
     return torch.cuda.device_count()
 
 
-def launch_replicas(n, argv, count_devices=visible_devices, python=sys.executable, script=None):
+def probe_device_count(python=sys.executable, timeout=600):
+    """GPU count for the LAUNCHER, from a throwaway child process, so the parent that spawns the
+    ranks never initialises HIP itself (torch's device count falls back to hipGetDeviceCount when
+    amdsmi fails). The child sees the same *_VISIBLE_DEVICES environment as the ranks will.
+    Returns None when the child gives no answer (the launcher then refuses to start ranks)."""
+    import subprocess
+
+    try:
+        r = subprocess.run([python, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True, timeout=timeout)
+        return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None
+    except (subprocess.SubprocessError, ValueError, IndexError, OSError):
+        return None
+
+
+def launch_replicas(n, argv, count_devices=probe_device_count, python=sys.executable, script=None, poll_s=0.2):
     """`bench.py --gpus N` without a torchrun environment: start N rank processes (RANK,
-    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT set; rank r drives device r) before anything touches
-    the GPU, wait for all of them and return the first non-zero exit status (0 if all passed).
-    Fewer than N visible devices is an error, not a silent N=1 run (one pair
+    LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT set; rank r drives device r) from a parent that has
+    not touched the GPU, and return the first non-zero exit status (0 if all passed). All ranks are
+    polled together: the first rank to fail ends the others at once (a rank that dies before the
+    gloo rendezvous would otherwise leave the rest waiting in it). Fewer than N visible devices, or
+    no device count at all, is an error (exit 2), not a silent N=1 run (one pair
     stream per GPU, the reference's pair loop demo/demo_mono.cpp:194-418 replicated)."""
     import subprocess
 
+    share = os.environ.get("BENCH_SHARE_DEVICE") == "1"
     have = count_devices()
-    if have < n and os.environ.get("BENCH_SHARE_DEVICE") != "1":
+    if have is None:
+        print(f"bench.py: --gpus {n}: could not count the visible GPUs (device-count probe failed)",
+              file=sys.stderr, flush=True)
+        return 2
+    if have < n and not (share and have >= 1):
         print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}", file=sys.stderr, flush=True)
         return 2
     port = str(_free_port())
@@ -93,9 +114,23 @@ def launch_replicas(n, argv, count_devices=visible_devices, python=sys.executabl
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([python, script or os.path.abspath(__file__)] + list(argv), env=env))
-    codes = [p.wait() for p in procs]
-    bad = [c for c in codes if c != 0]
-    return bad[0] if bad else 0
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and status == 0:
+                status = c
+                for q in live:  # the first failure ends the job
+                    q.terminate()
+        if live:
+            time.sleep(poll_s)
+    for p in procs:
+        p.wait()
+    return status
 
 
 def timed_region(run_steps, barrier, sync, reduce_max):
@@ -121,7 +156,9 @@ def timed_replays(torch, replay, stream, barrier, reduce_max, replays, local=Non
     holds the stream while the host submits them (sized from an untimed rehearsal of the host's
     submission time), so the GPU runs them back to back: the host's graph-launch cost at a short K
     (~0.1 ms per 20-node replay here, about the GPU time of the 20 calls) stays out of the events
-    instead of starving the GPU between calls."""
+    instead of starving the GPU between calls. The second value is the host's own submission time
+    per replay (launch + two event records), measured around the submission loop alone: the sleep
+    kernel's artificial backlog is not in it."""
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(replays)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(replays)]
 
@@ -147,17 +184,15 @@ def timed_replays(torch, replay, stream, barrier, reduce_max, replays, local=Non
 
     barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
     with torch.cuda.stream(stream):
         torch.cuda._sleep(int(cycles_per_s * (1.5 * host_s + 2e-3)))
-    submit()
+    host = submit() / replays
     torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) / replays
     barrier()
     med = statistics.median(s.elapsed_time(e) for s, e in zip(starts, ends)) * 1e-3
     if local is not None:
         local["median_s"] = med
-    return reduce_max(med), reduce_max(wall)
+    return reduce_max(med), reduce_max(host)
 
 
 def claim_stdout(ws):
@@ -341,20 +376,24 @@ def load_traffic(tag):
         return None
 
 
-def variants(torch, lightglue_amd, device, stream, q, k, v, flops):
+def variants(torch, lightglue_amd, device, stream, q, k, v, raw, flops):
     """BASELINE configs[2] and the plugin's Float boundary at the metric shape: fp16 in -> fp32 out
     (the reference's fp16in_fp32out kernel) and fp32 Q/K/V -> fp32 O (a TensorRT fp32 engine's
-    call: one launch, the inputs rounded to fp16 inside the 16-row kernel). Per-call time from a graph of 200 back-to-back calls, and the
-    max-abs error against a PyTorch fp32 attention of the same (fp16-valued) inputs on the GPU
-    (lightglue_pytorch_no_plugin/lightglue.py:82-84; north_star tolerance 1e-2)."""
+    call: one launch, the inputs rounded to fp16 inside the 16-row kernel). Per-call time from a
+    graph of 200 back-to-back calls, and the max-abs error against a PyTorch fp32 attention on the
+    GPU (lightglue_pytorch_no_plugin/lightglue.py:82-84; north_star tolerance 1e-2) of the inputs
+    each path receives: the fp16 Q/K/V for fp16in_fp32out, and for the Float boundary the RAW fp32
+    Q/K/V (`raw`, not fp16-representable), so its in-kernel RNE rounding is part of the error."""
     qf, kf, vf = (t.float() for t in (q, k, v))
-    ref = torch.softmax((qf @ kf.transpose(-1, -2)) * 0.125, -1) @ vf
+    ref16 = torch.softmax((qf @ kf.transpose(-1, -2)) * 0.125, -1) @ vf
+    qr, kr, vr = (torch.from_numpy(x).to(device).contiguous() for x in raw)
+    ref32 = torch.softmax((qr @ kr.transpose(-1, -2)) * 0.125, -1) @ vr
     o32 = torch.empty(q.shape, dtype=torch.float32, device=device)
-    of = torch.empty_like(qf)
+    of = torch.empty_like(qr)
     res = {}
-    for name, fn, o in (("fp16in_fp32out", lambda: lightglue_amd.mha_hd64_batched(q, k, v, out_dtype=torch.float32,
-                                                                                   out=o32), o32),
-                        ("float_boundary", lambda: lightglue_amd.mha_hd64(qf, kf, vf, out=of), of)):
+    for name, fn, o, ref in (("fp16in_fp32out", lambda: lightglue_amd.mha_hd64_batched(
+                                  q, k, v, out_dtype=torch.float32, out=o32), o32, ref16),
+                             ("float_boundary", lambda: lightglue_amd.mha_hd64(qr, kr, vr, out=of), of, ref32)):
         o.fill_(float("nan"))
         with torch.cuda.stream(stream):
             fn()
@@ -696,7 +735,11 @@ def main():
     if ws > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo")  # CPU barrier / timer reduce only; no RCCL on the data path
+        import datetime
+
+        # CPU barrier / timer reduce only; no RCCL on the data path. A bounded timeout: a rank that
+        # is gone fails the others' collectives within minutes instead of gloo's default 30.
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
     barrier, reduce_max = make_collectives(torch, dist)
 
     import lightglue_amd
@@ -784,7 +827,7 @@ def main():
                                                      "K-step graph; median over replays, max over ranks; replays "
                                                      "queued behind a sleep kernel so host submission does not gap "
                                                      "the GPU",
-                   "host_wall_ms_per_replay": round(wall * 1e3, 4),
+                   "host_submit_ms_per_replay": round(wall * 1e3, 4),
                    "calls_per_s_in_2000_step_graphs": long_rate},
         "per_rank_calls_per_s": rank_values,
         "outputs_bitwise_identical_across_ranks": len(set(digests)) == 1,
@@ -921,7 +964,8 @@ def main():
         result["roofline"]["saturated"] = {"form": f"{best_b} calls per launch (batched), best of 8 / 16 / 32",
                                            "frac": best, "frac_8_calls": result["batched"]["frac"]}
 
-        result["variants"] = variants(torch, lightglue_amd, device, stream, q, k, v, flops)
+        result["variants"] = variants(torch, lightglue_amd, device, stream, q, k, v, (qn, kn, vn), flops)
+        result["variants"]["float_boundary"]["inputs"] = "raw fp32 (synth.qkv), not fp16-representable"
         result["concurrent_streams"] = concurrent_streams(torch, lightglue_amd, device, nq, nkv, rank, flops)
         result["matcher_attention"] = matcher_attention(torch, device, stream, rank, separate=args.matcher_separate)
         result["matcher_e2e_fp16"] = matcher_e2e(torch, device, stream, rank)

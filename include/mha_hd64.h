@@ -135,8 +135,10 @@ size_t mha_hd64_get_workspace_size(const mha_hd64_plugin_t* p,
  *   HALF  -> fp16 in, fp32 accumulation, fp16 out   (reference: pad -> fp16in_fp16out kernel -> unpad)
  *   FLOAT -> fp32 in rounded to fp16 (RN) on load, fp32 accumulation, fp32 out
  *            (reference: convert+pad -> fp16in_fp32out kernel -> unpad)
- * One kernel launch on `stream`. At the reference's shapes with N <= 1024 (HALF) a workgroup
- * holds all keys of its 32 query rows (single-pass kernel, no split, no workspace use). A call
+ * One kernel launch on `stream`. At the reference's shapes with N <= 2048 (HALF) a workgroup
+ * holds all keys of its 16 query rows (the 16-row single-pass kernel: 256 workgroups for a
+ * 1x4x1024x1024 call, no split, no workspace use; 32-row blocks under a concurrency hint >= 2;
+ * FLOAT with N <= 1024 rounds fp32 to fp16 inside the same kernel, one launch). A call
  * whose keys are split across workgroups merges the
  * splits inside that launch through library-owned arrival tickets; the first enqueue on a
  * (device, stream) outside stream capture allocates them (and, once per device, a pre-zeroed
@@ -192,8 +194,13 @@ typedef struct mha_hd64_call {
 
 int32_t mha_hd64_launch_grouped(const mha_hd64_call_t* calls, int32_t n_calls, int32_t in_type,
                                 int32_t out_type, void* workspace, size_t ws_bytes, hipStream_t stream);
-/* Workspace bytes the grouped launcher can use (0 = no call of the group splits). */
+/* Workspace bytes the grouped launcher can use for fp16 inputs (0 = no call of the group splits). */
 size_t mha_hd64_grouped_workspace_bytes(const mha_hd64_call_t* calls, int32_t n_calls);
+/* The same for inputs of in_type (mha_hd64_dtype_t): for FLOAT groups that a single-pass kernel
+ * runs after a convert launch this includes the fp16 copies of Q/K/V; with less workspace such
+ * groups take the slower ring kernel (convert on load). The largest chunk of 4 calls counts
+ * (chunks reuse the workspace in stream order). 0 for an invalid in_type. */
+size_t mha_hd64_grouped_workspace_bytes_typed(const mha_hd64_call_t* calls, int32_t n_calls, int32_t in_type);
 
 /* ---- concurrency hint (no reference counterpart: TensorRT gives a plugin no view of its
  * other streams) ----

@@ -237,6 +237,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
 // be touched: every other row gains nothing, profiles/r02/prefetch_ab.txt); the returned dwords
 // are kept live until the caller's first wait covers them (oldest loads of the wave). Masked
 // lanes rather than out-of-range offsets: a full-wave load costs warm-input calls more.
+//
+// Register safety: the compiler does not track an asm load's pending VGPR write, so each load's
+// destination must stay the SAME register from the asm statement to the covering wait. No load is
+// therefore issued under a C-level branch (a join could merge the destination with its initial
+// value through a copy and hand the original register to another value while the load is in
+// flight): every statement is unconditional, the destination is a read-write ("+v") operand
+// initialised to 0, and lane selection is an EXEC mask applied and restored inside the statement
+// (waves other than the prefetching one run it with an empty mask).
 struct L2Prefetch {
     unsigned k[2] = {0u, 0u}, v[2] = {0u, 0u};
 };
@@ -245,18 +253,36 @@ __device__ __forceinline__ int prefetch_group(int total_blocks, int qtiles) {
     const int n = min(total_blocks >> 3, qtiles);
     return n >= 32 ? 32 : (n >= 16 ? 16 : 0);
 }
+// buffer_load_dword into `dst` on the lanes of `mask` only (EXEC saved and restored in the same
+// statement). `s_nop 4`: the descriptor / mask SGPRs may come straight from a VALU write
+// (readfirstlane, the ballot's v_cmp), which a VMEM / exec read must not follow within 5 states.
+__device__ __forceinline__ void masked_load_dword(unsigned& dst, unsigned off, __amdgpu_buffer_rsrc_t rs,
+                                                  unsigned long long mask) {
+    unsigned long long saved;
+    asm volatile(
+        "s_nop 4\n\t"
+        "s_and_saveexec_b64 %1, %4\n\t"
+        "buffer_load_dword %0, %2, %3, 0 offen\n\t"
+        "s_mov_b64 exec, %1"
+        : "+v"(dst), "=&s"(saved)
+        : "v"(off), "s"(rs), "s"(mask)
+        : "memory", "scc");
+}
+// `active`: wave-uniform (the prefetching wave); the other waves issue empty-mask statements.
 template <int WAVE_KEYS, int EARLY_KEYS>
 __device__ __forceinline__ void l2_prefetch(L2Prefetch& pf, __amdgpu_buffer_rsrc_t k_rs, __amdgpu_buffer_rsrc_t v_rs,
-                                            int nkv, int qtile, int group, int lane) {
-    if (group == 0) return;
+                                            int nkv, int qtile, int group, int lane, bool active) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {  // nkv <= 2048: at most 128 rows per workgroup
-        if (group * 64 * c >= nkv) break;
-        const int row = (qtile & (group - 1)) + group * (lane + 64 * c);
+        const int g = group > 0 ? group : 1;
+        const int row = (qtile & (g - 1)) + g * (lane + 64 * c);
         const unsigned off = (unsigned)row * 128u;
-        if (EARLY_KEYS < WAVE_KEYS && row < nkv && row % WAVE_KEYS >= EARLY_KEYS)
-            asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(pf.k[c]) : "v"(off), "s"(k_rs));
-        if (row < nkv) asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(pf.v[c]) : "v"(off), "s"(v_rs));
+        const bool live = active && group > 0 && row < nkv;
+        const unsigned long long mk =
+            __builtin_amdgcn_ballot_w64(EARLY_KEYS < WAVE_KEYS && live && row % WAVE_KEYS >= EARLY_KEYS);
+        const unsigned long long mv = __builtin_amdgcn_ballot_w64(live);
+        masked_load_dword(pf.k[c], off, k_rs, mk);
+        masked_load_dword(pf.v[c], off, v_rs, mv);
     }
 }
 __device__ __forceinline__ void l2_prefetch_done(L2Prefetch& pf) {

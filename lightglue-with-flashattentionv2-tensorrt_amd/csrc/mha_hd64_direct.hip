@@ -198,9 +198,8 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
         // L2 prefetch of the rows requested late (mha_hd64_device.h; profiles/r02/prefetch_ab.txt)
         L2Prefetch pf;
         if constexpr (MHA_D_PREFETCH != 0 && !(MHA_ABL & ABL_NO_GLOAD))
-            if (wave == 0)
-                l2_prefetch<WAVE_KEYS, kTileKV * KFIRST>(pf, k_rs, v_rs, nkv, qtile,
-                                                         prefetch_group(a.total_blocks, ca.qtiles), lane);
+            l2_prefetch<WAVE_KEYS, kTileKV * KFIRST>(pf, k_rs, v_rs, nkv, qtile,
+                                                     prefetch_group(a.total_blocks, ca.qtiles), lane, wave == 0);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             if (MHA_ABL & ABL_NO_GLOAD) qraw[s] = f16x8{} + (f16)(lane * 0.01f);

@@ -399,9 +399,8 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         // L2-resident inputs +0.02 us (4.65); at 768^2 / 1024x2048 -15 / -22 % cold, +2 % warm.
         L2Prefetch pf;
         if constexpr (MHA_D16_PREFETCH != 0)
-            if (wave == 0)
-                l2_prefetch<WAVE_KEYS, 2 * kTileKV>(pf, k_rs, v_rs, nkv, qtile,  // K(0), K(1) at entry
-                                                    prefetch_group(total_blocks, ca.qtiles), lane);
+            l2_prefetch<WAVE_KEYS, 2 * kTileKV>(pf, k_rs, v_rs, nkv, qtile,  // K(0), K(1) at entry
+                                                prefetch_group(total_blocks, ca.qtiles), lane, wave == 0);
         if constexpr (K0F) dma_k(0, 1);
 #pragma unroll
         for (int s = 0; s < 2; ++s)

@@ -63,7 +63,10 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
 hipError_t launch_group(const Call* calls, int n, InType in, OutType out, void* workspace, size_t ws_bytes,
                         hipStream_t stream, int force_q_waves = 0, int force_kv_waves = 0, int force_splits = 0,
                         int phase_mask = 3);
-size_t group_workspace_bytes(const Call* calls, int n);
+// Workspace bytes launch_group can use for these calls with inputs of type `in`: the largest
+// chunk's need (chunks of kGroupCalls reuse the workspace in stream order) -- split partials, or
+// for fp32 inputs the fp16 copies the convert launch writes when a single-pass kernel runs them.
+size_t group_workspace_bytes(const Call* calls, int n, InType in = InType::F16);
 
 // Workgroup shapes compiled: (q_waves, kv_waves) in {(4,1), (2,2), (1,2), (4,2)} with 32-row waves,
 // and (2,2) with 64-row waves (forced as q_waves = 12).

@@ -894,8 +894,12 @@ void set_stamp_buffer(void* p) { g_stamps = reinterpret_cast<unsigned long long*
 //    stream may be replayed side by side).
 // Arrays are created only outside capture (hipMalloc + memset, then a one-time stream sync for the
 // arena); a launch that finds no tickets combines in the second kernel instead. Nothing is freed
-// (a launch in flight or a graph may still reference it); a half-used arena is replaced at the
-// next eager launch (tickets_for).
+// (a launch in flight or a graph may still reference it). A half-used arena is replaced at the
+// next eager launch (tickets_for), at most kMaxArenas times per device: memory for tickets is
+// bounded by (kMaxArenas + 1) x 4 MiB per device plus the per-stream arrays; past the cap, captures
+// that find the arena full use the combine kernel (same bits). So an EAGER split launch may
+// allocate device memory (never more than that bound); it does so with this thread's capture mode
+// exchanged to relaxed, so a global-mode capture running on another thread stays valid.
 namespace {
 int g_fused = -1;  // -1: unset (env MHA_HD64_FUSED_COMBINE, default on), 0 off, 1 on
 std::mutex g_ticket_mu;
@@ -904,10 +908,19 @@ struct Arena {
     unsigned* base = nullptr;
     int cap = 0;
     int used = 0;
+    int replaced = 0;
 };
 std::map<int, Arena> g_arena;
 thread_local int g_last_combine = 0;  // this thread's last launch: 0 no split, 1 in-launch, 2 kernel
 constexpr int kArenaTickets = 1 << 20;  // 4 MiB per device
+constexpr int kMaxArenas = 4;           // replacements per device
+// Scoped relaxed capture mode for this thread: allocation calls stay legal (and do not invalidate
+// another thread's global-mode capture) while any capture is in progress in the process.
+struct RelaxedCapture {
+    hipStreamCaptureMode prev = hipStreamCaptureModeRelaxed;
+    RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&prev); }
+    ~RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&prev); }
+};
 }  // namespace
 
 int last_combine_form() { return g_last_combine; }
@@ -958,9 +971,11 @@ static unsigned* tickets_for(hipStream_t stream, int count) {
     }
     // First eager launch on this device: the arena for later captures. An arena more than half
     // carved is replaced by a fresh one at the next eager launch (the old one stays allocated: graphs
-    // recorded from it may still run), so captures run out only after 512 Ki tickets recorded with
-    // no eager launch in between.
-    if (!ar.base || ar.used > ar.cap / 2) {
+    // recorded from it may still run), at most kMaxArenas times, so captures run out only after
+    // 512 Ki tickets recorded with no eager launch in between.
+    RelaxedCapture relaxed;
+    if (!ar.base || (ar.used > ar.cap / 2 && ar.replaced < kMaxArenas)) {
+        if (ar.base) ++ar.replaced;
         unsigned* fresh = zeroed_tickets(kArenaTickets, stream);
         if (fresh && hipStreamSynchronize(stream) == hipSuccess) {
             ar.base = fresh;
@@ -1403,10 +1418,31 @@ hipError_t launch_group(const Call* calls, int n, InType in, OutType out, void* 
     return hipSuccess;
 }
 
-size_t group_workspace_bytes(const Call* calls, int n) {
+// What launch_group_chunk uses for one chunk (same decisions, in the same order).
+static size_t chunk_workspace_bytes(const Call* calls, int n, InType in) {
+    if (in == InType::F32 && f32_convert_enabled()) {
+        const GroupPlan p16 = plan_group(calls, n, 0, 0, 0, 0, InType::F16);
+        const bool in32_direct = f32_inkernel_enabled() && p16.direct_tiles > 0 && p16.direct_tiles <= 2 &&
+                                 p16.rows_per_wave == 16;
+        if (in32_direct) return 0;
+        if (p16.direct_tiles > 0) {  // convert launch into the workspace, then the fp16 single-pass kernel
+            size_t off = 0;
+            for (int i = 0; i < n; ++i) {
+                if (calls[i].nq <= 0 || calls[i].batch <= 0 || calls[i].heads <= 0) continue;
+                const size_t bh = (size_t)calls[i].batch * calls[i].heads;
+                off += align256(bh * calls[i].nq * kHeadDim * sizeof(f16)) +
+                       2 * align256(bh * calls[i].nkv * kHeadDim * sizeof(f16));
+            }
+            return off;
+        }
+    }
+    return plan_group(calls, n, (size_t)-1, 0, 0, 0, in).ws_needed;
+}
+
+size_t group_workspace_bytes(const Call* calls, int n, InType in) {
     size_t need = 0;
     for (int i = 0; i < n; i += kMaxCalls)
-        need = std::max(need, plan_group(calls + i, std::min(kMaxCalls, n - i), (size_t)-1).ws_needed);
+        need = std::max(need, chunk_workspace_bytes(calls + i, std::min(kMaxCalls, n - i), in));
     return need;
 }
 

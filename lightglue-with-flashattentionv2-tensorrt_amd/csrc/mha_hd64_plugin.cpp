@@ -345,9 +345,16 @@ int32_t mha_hd64_launch_grouped(const mha_hd64_call_t* calls, int32_t n_calls, i
 }
 
 size_t mha_hd64_grouped_workspace_bytes(const mha_hd64_call_t* calls, int32_t n_calls) {
+    return mha_hd64_grouped_workspace_bytes_typed(calls, n_calls, MHA_HD64_DT_HALF);
+}
+
+size_t mha_hd64_grouped_workspace_bytes_typed(const mha_hd64_call_t* calls, int32_t n_calls, int32_t in_type) {
+    if (in_type != MHA_HD64_DT_HALF && in_type != MHA_HD64_DT_FLOAT) return 0;
     std::vector<mha_hd64::Call> v;
     if (to_calls(calls, n_calls, v) != MHA_HD64_STATUS_SUCCESS || v.empty()) return 0;
-    return mha_hd64::group_workspace_bytes(v.data(), (int)v.size());
+    return mha_hd64::group_workspace_bytes(v.data(), (int)v.size(),
+                                           in_type == MHA_HD64_DT_FLOAT ? mha_hd64::InType::F32
+                                                                        : mha_hd64::InType::F16);
 }
 
 // ---- diagnostics ----

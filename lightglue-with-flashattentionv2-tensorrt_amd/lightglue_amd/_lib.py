@@ -115,6 +115,7 @@ SIGNATURES = {
     "mha_hd64_launch_workspace_bytes": ([_I, _I, _I, _I], _S),
     "mha_hd64_launch_grouped": ([ctypes.POINTER(CallDesc), _I, _I, _I, _P, _S, _P], _I),
     "mha_hd64_grouped_workspace_bytes": ([ctypes.POINTER(CallDesc), _I], _S),
+    "mha_hd64_grouped_workspace_bytes_typed": ([ctypes.POINTER(CallDesc), _I, _I], _S),
     "mha_hd64_set_concurrency_hint": ([_I], _I),
     "mha_hd64_last_error": ([], _C),
     "mha_hd64_set_abort_on_error": ([_I], None),

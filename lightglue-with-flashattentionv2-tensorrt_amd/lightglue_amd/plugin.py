@@ -326,13 +326,9 @@ def mha_hd64_grouped(calls, out_dtype=None, outs=None):
     lib = _lib.load()
     device = calls[0][0].device
     stream = torch.cuda.current_stream(device).cuda_stream
-    nbytes = lib.mha_hd64_grouped_workspace_bytes(descs, len(calls))
-    if in_dtype == torch.float32:
-        # room for the fp16 copies of Q/K/V that the convert launch writes when a single-pass
-        # kernel the planner picks does not round fp32 inputs itself (nkv > 1024); without it
-        # such groups fall back to the ring kernel's slower convert-on-load
-        a256 = lambda n: (2 * n + 255) // 256 * 256  # noqa: E731
-        nbytes = max(nbytes, sum(a256(q.numel()) + 2 * a256(k.numel()) for q, k, _ in calls))
+    # (fp32 groups: includes the fp16 copies of Q/K/V the convert launch writes when a single-pass
+    # kernel that does not round fp32 inputs itself runs them; largest chunk of 4 calls)
+    nbytes = lib.mha_hd64_grouped_workspace_bytes_typed(descs, len(calls), _DT[in_dtype])
     ws = _workspace(device, stream, nbytes) if nbytes else None
     status = lib.mha_hd64_launch_grouped(descs, len(calls), _DT[in_dtype], _DT[out_dtype],
                                          ws.data_ptr() if ws is not None else None, nbytes, stream)

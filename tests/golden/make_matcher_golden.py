@@ -2,7 +2,7 @@
 
 Run in the build container only (it reads /root/reference, absent on the GPU box):
 
-    python tests/golden/make_matcher_golden.py
+    python tests/golden/make_matcher_golden.py [name ...]    (no names: every case)
 
 Builds the reference model ``LightGlue(features=None, n_layers=L)`` from
 /root/reference/lightglue_pytorch_no_plugin/lightglue.py (module file loaded directly; the
@@ -44,6 +44,8 @@ CASES = {
 # name: (seed, n_layers, m, n, overlap, row_stride)
 SWEEP_CASES = {
     "sweep_l9_512x512": (11, 9, 512, 512, 384, 16),
+    "sweep_l9_1024x1024": (12, 9, 1024, 1024, 768, 32),
+    "sweep_l9_2048x2048": (13, 9, 2048, 2048, 1536, 64),
 }
 
 
@@ -57,13 +59,27 @@ def digest(sd, pair) -> str:
     return h.hexdigest()
 
 
+def _merge_index(path, new):
+    old = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            old = json.load(f)
+    old.update(new)
+    with open(path, "w") as f:
+        json.dump(old, f, indent=1, sort_keys=True)
+
+
 def main():
+    want = set(sys.argv[1:])
+    pick = lambda name: not want or name in want  # noqa: E731
     spec = importlib.util.spec_from_file_location("lg_ref", REF)
     lg = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(lg)
     torch.manual_seed(0)
     index = {}
     for name, (seed, layers, m, n) in CASES.items():
+        if not pick(name):
+            continue
         model = lg.LightGlue(features=None, n_layers=layers).eval()
         sd = matcher.seeded_state_dict(seed, layers)
         model.load_state_dict(sd, strict=True)
@@ -80,10 +96,11 @@ def main():
         index[name] = {"seed": seed, "n_layers": layers, "m": m, "n": n, "inputs_sha256": digest(sd, pair),
                        "n_matches": int(matches.shape[0])}
         print(name, {k: v.shape for k, v in out.items()}, "matches", int(matches.shape[0]))
-    with open(os.path.join(HERE, "matcher_index.json"), "w") as f:
-        json.dump(index, f, indent=1, sort_keys=True)
+    _merge_index(os.path.join(HERE, "matcher_index.json"), index)
     sweep = {}
     for name, (seed, layers, m, n, overlap, stride) in SWEEP_CASES.items():
+        if not pick(name):
+            continue
         model = lg.LightGlue(features=None, n_layers=layers).eval()
         sd = matcher.seeded_state_dict(seed, layers)
         model.load_state_dict(sd, strict=True)
@@ -104,8 +121,7 @@ def main():
                        "inputs_sha256": digest(sd, pair), "n_matches": int(matches.shape[0]),
                        "n_matches_all": int(matches_all.shape[0])}
         print(name, "matches", int(matches.shape[0]), "mutual", int(matches_all.shape[0]))
-    with open(os.path.join(HERE, "matcher_sweep_index.json"), "w") as f:
-        json.dump(sweep, f, indent=1, sort_keys=True)
+    _merge_index(os.path.join(HERE, "matcher_sweep_index.json"), sweep)
 
 
 if __name__ == "__main__":

@@ -105,6 +105,52 @@ def test_launcher_refuses_missing_devices(capsys):
     assert "--gpus 8 needs 8 visible GPUs, found 1" in capsys.readouterr().err
 
 
+def test_launcher_refuses_when_device_count_unknown(capsys):
+    """The launcher never falls back to counting devices in its own process (that would initialise
+    HIP in the parent that spawns the ranks): a failed probe is exit 2 with a message."""
+    import bench
+
+    called = []
+    assert bench.launch_replicas(2, [], count_devices=lambda: None, script="/nonexistent") == 2
+    assert "could not count the visible GPUs" in capsys.readouterr().err
+    assert not called
+
+
+def test_device_probe_runs_in_a_child(monkeypatch):
+    """probe_device_count() answers from a child process; a broken interpreter gives None."""
+    import bench
+
+    n = bench.probe_device_count()
+    assert n == torch.cuda.device_count()
+    assert bench.probe_device_count(python="/nonexistent/python") is None
+
+
+_SLOW_RANK = r"""
+import os, sys, time
+rank = int(os.environ["RANK"])
+if rank == 0:
+    sys.exit(5)          # dies before any rendezvous
+time.sleep(120)          # would wait in the rendezvous for the default timeout
+"""
+
+
+def test_launcher_ends_the_job_at_the_first_failure(tmp_path):
+    import time
+
+    import bench
+
+    script = tmp_path / "slow.py"
+    script.write_text(_SLOW_RANK)
+    env_ws = os.environ.pop("WORLD_SIZE", None)
+    try:
+        t0 = time.time()
+        assert bench.launch_replicas(3, [], count_devices=lambda: 3, script=str(script)) == 5
+        assert time.time() - t0 < 30
+    finally:
+        if env_ws is not None:
+            os.environ["WORLD_SIZE"] = env_ws
+
+
 def test_bench_gpus2_fails_loudly_without_devices():
     """The driver's `python bench.py --gpus 2` on a box with fewer GPUs exits non-zero with a message."""
     import subprocess
@@ -163,3 +209,25 @@ def test_claim_stdout_keeps_only_the_json_line():
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip() == '{"metric": 1}'
     assert "Gloo" in r.stderr and "noise from python" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_hardware():
+    """The N>1 path on the GPU box: `BENCH_SHARE_DEVICE=1 bench.py --gpus 2 --quick` (two rank
+    processes sharing the one GPU, gloo group, per-rank rates, cross-rank output digest). Exactly one
+    JSON line on stdout."""
+    import json
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["BENCH_SHARE_DEVICE"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--quick", "--steps", "200",
+                        "--warmup", "20"], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert len(d["per_rank_calls_per_s"]) == 2 and all(v > 0 for v in d["per_rank_calls_per_s"])
+    assert d["outputs_bitwise_identical_across_ranks"] is True
