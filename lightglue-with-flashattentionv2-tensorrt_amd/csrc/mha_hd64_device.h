@@ -60,6 +60,10 @@ hipError_t launch_direct(const FwdArgs& a, int grid, int tiles_per_wave, bool ou
 // in_f32: fp32 Q/K/V rounded to fp16 inside the kernel (tiles_per_wave <= 2 only).
 hipError_t launch_direct16(const FwdArgs& a, int grid, int tiles_per_wave, bool out_f32, hipStream_t stream,
                            bool in_f32 = false);
+// Persistent streaming kernel (mha_hd64_stream.hip): 128-row items, all keys, fp16 Q/K/V;
+// a.total_blocks = items (128-row blocks of every call, qtiles per call of 128 rows).
+hipError_t launch_stream(const FwdArgs& a, bool out_f32, hipStream_t stream);
+int stream_grid(int items);
 
 namespace {
 // Uniform (scalar) selection of call ci's arguments from the kernarg table (grouped launches).

@@ -37,6 +37,7 @@ struct LaunchPlan {
     int tiles_per_split;  // KV super-tiles (64 * kv_waves keys) per split
     size_t ws_needed;     // workspace bytes the plan uses
     int direct_tiles;     // > 0: single-pass kernel, 8 waves x direct_tiles 64-key tiles (no split)
+    int stream;           // 1: the persistent streaming kernel (128-row items, no split)
 };
 
 // Up to kGroupCalls calls share one launch (grouped launcher); larger groups are chunked.
@@ -53,11 +54,14 @@ struct GroupPlan {
     size_t ws_offset[kGroupCalls];
     size_t ws_needed;
     int direct_tiles;  // > 0: the single-pass kernel (mha_hd64_direct.hip), q_waves 1 x kv_waves 8
+    int stream;        // 1: the persistent streaming kernel (mha_hd64_stream.hip), 128-row items
 };
 // force_q_waves = kForceDirect selects the single-pass kernel (fp16 input, nkv <= 1024).
 constexpr int kForceDirect = 21;
 // force_q_waves = kForceDirect16 selects the 16-row single-pass kernel (mha_hd64_direct16.hip).
 constexpr int kForceDirect16 = 22;
+// force_q_waves = kForceStream selects the persistent streaming kernel (mha_hd64_stream.hip).
+constexpr int kForceStream = 23;
 GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_waves = 0, int force_kv_waves = 0,
                      int force_splits = 0, InType in = InType::F16);
 hipError_t launch_group(const Call* calls, int n, InType in, OutType out, void* workspace, size_t ws_bytes,

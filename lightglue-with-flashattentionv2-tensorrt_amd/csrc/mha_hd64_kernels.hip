@@ -1051,9 +1051,39 @@ static bool direct16_enabled() {
     return on;
 }
 
+// The persistent streaming kernel (mha_hd64_stream.hip) for launches of many 128-row blocks
+// (MHA_HD64_STREAM=0: never, 1: for every fp16 launch past one round of 16-row blocks).
+static int stream_env() {
+    static const int v = [] {
+        const char* e = std::getenv("MHA_HD64_STREAM");
+        return e ? (e[0] == '0' ? 0 : 1) : -1;
+    }();
+    return v;
+}
+static bool stream_auto(const Call* calls, int n, InType in) {
+    if (in != InType::F16 || stream_env() <= 0) return false;
+    long blocks128 = 0;
+    for (int i = 0; i < n; ++i) blocks128 += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 127) / 128);
+    return blocks128 > 256;
+}
+
 GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_waves, int force_kv_waves,
                      int force_splits, InType in) {
     GroupPlan p{};
+    if (force_q_waves == kForceStream || (force_q_waves == 0 && stream_auto(calls, n, in))) {
+        if (in == InType::F16) {
+            p.q_waves = 4;
+            p.kv_waves = 1;
+            p.rows_per_wave = 32;
+            p.stream = 1;
+            for (int i = 0; i < n; ++i) {
+                p.splits[i] = 1;
+                p.tiles_per_split[i] = 1;
+            }
+            return p;
+        }
+        force_q_waves = 0;  // fp32 inputs: the planner's choice
+    }
     // 16-row blocks first: a launch of at most 256 of them runs every block on its own CU. Under a
     // concurrency hint >= 2 (several streams of independent calls) a call takes 32-row blocks on
     // half the CUs instead (launch_direct: two-per-CU form from hint 3), so the streams overlap.
@@ -1191,6 +1221,7 @@ LaunchPlan plan_call(const Call& c, size_t ws_bytes, int force_q_waves, int forc
     p.tiles_per_split = g.tiles_per_split[0];
     p.ws_needed = g.ws_needed;
     p.direct_tiles = g.direct_tiles;
+    p.stream = g.stream;
     return p;
 }
 
@@ -1253,7 +1284,8 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
 static hipError_t launch_f32_via_f16(const Call* calls, int n, OutType out, void* workspace, size_t ws_bytes,
                                      hipStream_t stream, int phase_mask) {
     if (!f32_convert_enabled() || !workspace) return hipErrorNotSupported;
-    if (plan_group(calls, n, 0, 0, 0, 0, InType::F16).direct_tiles == 0) return hipErrorNotSupported;
+    const GroupPlan p16 = plan_group(calls, n, 0, 0, 0, 0, InType::F16);
+    if (p16.direct_tiles == 0 && !p16.stream) return hipErrorNotSupported;
     Call c16[kMaxCalls];
     ConvArgs cv{};
     size_t off = 0;
@@ -1349,6 +1381,11 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
     a.n_calls = n_live;
     a.total_blocks = blocks;
     const int rbw = p.rows_per_wave / 32;
+    if (p.stream) {  // persistent streaming kernel: no split, no workspace
+        g_last_combine = 0;
+        if (!(phase_mask & 1)) return hipSuccess;
+        return launch_stream(a, out == OutType::F32, stream);
+    }
     if (p.direct_tiles > 0) {  // single-pass kernel: no split, no workspace
         g_last_combine = 0;
         if (!(phase_mask & 1)) return hipSuccess;
@@ -1425,7 +1462,7 @@ static size_t chunk_workspace_bytes(const Call* calls, int n, InType in) {
         const bool in32_direct = f32_inkernel_enabled() && p16.direct_tiles > 0 && p16.direct_tiles <= 2 &&
                                  p16.rows_per_wave == 16;
         if (in32_direct) return 0;
-        if (p16.direct_tiles > 0) {  // convert launch into the workspace, then the fp16 single-pass kernel
+        if (p16.direct_tiles > 0 || p16.stream) {  // convert launch into the workspace, then the fp16 kernel
             size_t off = 0;
             for (int i = 0; i < n; ++i) {
                 if (calls[i].nq <= 0 || calls[i].batch <= 0 || calls[i].heads <= 0) continue;

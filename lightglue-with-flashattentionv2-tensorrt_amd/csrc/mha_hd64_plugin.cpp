@@ -382,17 +382,20 @@ int32_t mha_hd64_launch_forced(const void* q, const void* k, const void* v, void
     const mha_hd64::LaunchPlan plan =
         mha_hd64::plan_call(c, workspace ? ws_bytes : 0, q_waves, kv_waves, splits,
                             in_f32 ? mha_hd64::InType::F32 : mha_hd64::InType::F16);
-    const int plan_qw = plan.direct_tiles > 0
+    const int plan_qw = plan.stream ? mha_hd64::kForceStream
+                        : plan.direct_tiles > 0
                             ? (plan.rows_per_wave == 16 ? mha_hd64::kForceDirect16 : mha_hd64::kForceDirect)
                             : plan.q_waves + (plan.rows_per_wave == 64 ? 10 : 0);
     // (2,4), (1,4), (1,8) take one split per super-tile and fall back to (2,2) past 16 of them
     const bool single_tile = kv_waves >= 4;
     const bool fell_back = single_tile && plan_qw == 2 && plan.kv_waves == 2;
     // q_waves = 21 / 22 force the 32- / 16-row single-pass kernel (kv_waves / splits ignored)
-    const bool direct = q_waves == mha_hd64::kForceDirect || q_waves == mha_hd64::kForceDirect16;
+    // q_waves = 23 forces the persistent streaming kernel (fp16 input)
+    const bool direct = q_waves == mha_hd64::kForceDirect || q_waves == mha_hd64::kForceDirect16 ||
+                        q_waves == mha_hd64::kForceStream;
     if (direct && plan_qw != q_waves)
         return fail(MHA_HD64_STATUS_BAD_PARAM, __FILE__, __LINE__,
-                    "single-pass kernel: fp16 input, nkv <= 1024 (16-row) / 2048 (32-row)");
+                    "single-pass / streaming kernel: fp16 input, nkv <= 1024 (16-row) / 2048 (32-row)");
     if (q_waves != 0 && !direct && !fell_back && (plan_qw != q_waves || plan.kv_waves != kv_waves))
         return fail(MHA_HD64_STATUS_BAD_PARAM, __FILE__, __LINE__, "forced workgroup shape is not compiled");
     if (splits > 1 && !single_tile && !direct && plan.splits != splits)
@@ -420,8 +423,9 @@ size_t mha_hd64_plan(int32_t batch, int32_t heads, int32_t nq, int32_t nkv, size
     const mha_hd64::Call c{nullptr, nullptr, nullptr, nullptr, batch, heads, nq, nkv};
     const mha_hd64::LaunchPlan p = mha_hd64::plan_call(c, ws_bytes);
     if (out4) {
-        out4[0] = p.direct_tiles > 0 ? (p.rows_per_wave == 16 ? mha_hd64::kForceDirect16 : mha_hd64::kForceDirect)
-                                     : p.q_waves + (p.rows_per_wave == 64 ? 10 : 0);
+        out4[0] = p.stream ? mha_hd64::kForceStream
+                  : p.direct_tiles > 0 ? (p.rows_per_wave == 16 ? mha_hd64::kForceDirect16 : mha_hd64::kForceDirect)
+                                       : p.q_waves + (p.rows_per_wave == 64 ? 10 : 0);
         out4[1] = p.kv_waves;
         out4[2] = p.splits;
         out4[3] = p.tiles_per_split;
