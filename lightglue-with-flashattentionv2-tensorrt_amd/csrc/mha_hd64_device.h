@@ -62,8 +62,9 @@ hipError_t launch_direct16(const FwdArgs& a, int grid, int tiles_per_wave, bool 
                            bool in_f32 = false);
 // Persistent streaming kernel (mha_hd64_stream.hip): 128-row items, all keys, fp16 Q/K/V;
 // a.total_blocks = items (128-row blocks of every call, qtiles per call of 128 rows).
-hipError_t launch_stream(const FwdArgs& a, bool out_f32, hipStream_t stream);
-int stream_grid(int items);
+// waves = 4 (128-row items, two workgroups per CU) or 8 (256-row items, one per CU).
+hipError_t launch_stream(const FwdArgs& a, int waves, bool out_f32, hipStream_t stream);
+int stream_grid(int items, int waves);
 
 namespace {
 // Uniform (scalar) selection of call ci's arguments from the kernarg table (grouped launches).
@@ -230,6 +231,33 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
 }
+
+// One 1-KiB LDS-DMA piece (`buffer_load_dwordx4 … lds`: 64 lanes x 16 B from rs at voff + soff
+// into LDS [m0, m0 + 1 KiB)) as inline asm, M0 written inside the statement. The compiler does not
+// see this LDS write, so it adds no wait of its own: every read of the destination must follow the
+// issuing wave's counted vmcnt (and a barrier for other waves' reads). (With the LDS-DMA builtin
+// the compiler cannot tell the DMA's LDS writes from later ds_read_b64_tr_b16 reads of any address
+// and drains EVERY DMA in flight, vmcnt(0), before the first transposing read.)
+// m0 / soff are wave-uniform; readfirstlane pins values the compiler computed on the vector unit
+// into the SGPRs the "s" constraints need.
+__device__ __forceinline__ void lds_dma16(unsigned m0, unsigned voff, __amdgpu_buffer_rsrc_t rs, unsigned soff) {
+    m0 = __builtin_amdgcn_readfirstlane(m0);
+    soff = __builtin_amdgcn_readfirstlane(soff);
+    asm volatile(
+        "s_mov_b32 m0, %0\n\t"
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %3 offen lds"
+        :
+        : "s"(m0), "v"(voff), "s"(rs), "s"(soff)
+        : "memory");
+}
+// LDS byte address of a pointer into a __shared__ array (the value M0 takes)
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+#ifndef MHA_DMA_ASM
+#define MHA_DMA_ASM 1  // 0: the LDS-DMA builtin in the single-pass kernels (A/B hook)
+#endif
 
 // L2 prefetch for the single-pass kernels (issued by one wave per workgroup, before its own
 // loads). A workgroup's DMA requests K of its first tiles at entry but V tile by tile once K(t)

@@ -359,8 +359,15 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         const unsigned v_lane_off = lrow + (((lane & 7) ^ (((lane >> 4) & 3) << 1)) << 4);
         // source piece i of the wave's key slice into region piece li (li = i except in pass 1)
         auto dma_piece = [&](__amdgpu_buffer_rsrc_t rs, unsigned voff, int i, int li) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * li),
-                                                     16, voff, 1024 * i, 0, 0);
+            // asm DMA in the multi-pass forms (no compiler drain before the transposing reads:
+            // 1x4x1024x2048 7.28 vs 7.64 us); the one-pass forms measured neutral (1024^2 5.02 vs
+            // 5.00, 768^2 4.48 vs 4.28) and keep the builtin
+            if (MHA_DMA_ASM && PASSES > 1) {
+                lds_dma16(lds_addr(smem + region + 1024 * li), voff, rs, 1024u * i);
+            } else {
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(smem + region + 1024 * li),
+                                                         16, voff, 1024 * i, 0, 0);
+            }
         };
         auto dma_k = [&](int t0, int t1) {
 #pragma unroll

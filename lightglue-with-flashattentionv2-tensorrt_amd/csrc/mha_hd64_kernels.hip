@@ -1060,6 +1060,14 @@ static int stream_env() {
     }();
     return v;
 }
+// waves per streaming workgroup (MHA_HD64_STREAM_WAVES=4 or 8; A/B switch)
+static int stream_waves() {
+    static const int v = [] {
+        const char* e = std::getenv("MHA_HD64_STREAM_WAVES");
+        return (e && e[0] == '4') ? 4 : 8;
+    }();
+    return v;
+}
 static bool stream_auto(const Call* calls, int n, InType in) {
     if (in != InType::F16 || stream_env() <= 0) return false;
     long blocks128 = 0;
@@ -1072,7 +1080,7 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
     GroupPlan p{};
     if (force_q_waves == kForceStream || (force_q_waves == 0 && stream_auto(calls, n, in))) {
         if (in == InType::F16) {
-            p.q_waves = 4;
+            p.q_waves = stream_waves();  // 128- or 256-row items
             p.kv_waves = 1;
             p.rows_per_wave = 32;
             p.stream = 1;
@@ -1384,7 +1392,7 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
     if (p.stream) {  // persistent streaming kernel: no split, no workspace
         g_last_combine = 0;
         if (!(phase_mask & 1)) return hipSuccess;
-        return launch_stream(a, out == OutType::F32, stream);
+        return launch_stream(a, p.q_waves, out == OutType::F32, stream);
     }
     if (p.direct_tiles > 0) {  // single-pass kernel: no split, no workspace
         g_last_combine = 0;

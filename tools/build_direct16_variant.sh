@@ -16,7 +16,7 @@ if [ "$WITH_DIRECT" = 1 ]; then
         "$@" -I../include -Icsrc -c csrc/mha_hd64_direct.hip -o lib/exp/d32_$NAME.o
   DOBJ=lib/exp/d32_$NAME.o
 fi
-hipcc --offload-arch=gfx950 -shared -fPIC lib/obj/mha_hd64_kernels.o $DOBJ lib/exp/d16_$NAME.o \
+hipcc --offload-arch=gfx950 -shared -fPIC lib/obj/mha_hd64_kernels.o $DOBJ lib/exp/d16_$NAME.o lib/obj/mha_hd64_stream.o \
       lib/obj/mha_hd64_plugin.o lib/obj/lightglue_glue.o lib/obj/lightglue_linear.o -o lib/exp/libmha_hd64_$NAME.so
 rm -f lib/exp/d16_$NAME.o lib/exp/d32_$NAME.o
 echo lib/exp/libmha_hd64_$NAME.so

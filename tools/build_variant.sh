@@ -9,7 +9,7 @@ mkdir -p lib/exp
 make -s lib/libmha_hd64.so
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans "$@" \
       -I../include -Icsrc -c "$SRC" -o lib/exp/k_$NAME.o
-PLUG="lib/obj/mha_hd64_plugin.o lib/obj/lightglue_glue.o lib/obj/lightglue_linear.o lib/obj/mha_hd64_direct.o lib/obj/mha_hd64_direct16.o"
+PLUG="lib/obj/mha_hd64_plugin.o lib/obj/lightglue_glue.o lib/obj/lightglue_linear.o lib/obj/mha_hd64_direct.o lib/obj/mha_hd64_direct16.o lib/obj/mha_hd64_stream.o"
 if [ -n "$PLUGIN_SRC" ]; then  # an older plugin shim for an older kernel source
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Icsrc -c "$(readlink -f "$PLUGIN_SRC")" -o lib/exp/p_$NAME.o
   PLUG=lib/exp/p_$NAME.o
