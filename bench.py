@@ -884,6 +884,7 @@ def main():
         t_call = statistics.median(event_durations_ms(torch, full_call, 200, stream)[20:])
         achieved = flops / (t_main * 1e-3) / 1e12
         mfma_busy = load_traffic("direct16_mfma_busy_cycles_per_simd")
+        rocprof_ns = load_traffic("direct16_rocprof_avg_ns")
         traffic = load_traffic({22: "direct16_kernel_bytes_per_launch", 21: "direct_kernel_bytes_per_launch"}.get(
             q_waves, "main_kernel_bytes_per_launch"))
         two = " in two passes of 4 tiles" if nkv > 1024 else ""
@@ -903,6 +904,11 @@ def main():
                                    else round(mfma_busy / (t_main * 1e-3 * 2.4e9), 4)),
             "kernel": kname,
             "kernel_us": round(t_main * 1e3, 3),
+            # the same kernel's average duration in the committed rocprofv3 --kernel-trace --stats
+            # summary of `bench.py --only call` (eager launches, profiler in the loop), as a frac
+            "frac_rocprof_avg": (None if rocprof_ns is None or q_waves != 22
+                                 else round(flops / (rocprof_ns * 1e-9) / 1e12 / PEAK_F16_TFLOPS, 4)),
+            "rocprof_avg_us": None if rocprof_ns is None or q_waves != 22 else round(rocprof_ns * 1e-3, 3),
             "direct32_kernel_us": None if t_direct32 is None else round(t_direct32 * 1e3, 3),
             "ring_split_plan_us": {"in_launch_combine": round(t_ring * 1e3, 3), "main": round(t_main2 * 1e3, 3),
                                    "combine": round(t_comb2 * 1e3, 3), "two_kernels": round(t_two * 1e3, 3)},
@@ -945,6 +951,17 @@ def main():
             t2 = graph_per_launch_ms(torch, lambda: lightglue_amd.mha_hd64_batched(qs, ks, vs, out=os_), stream, k=50)
             sweep_b[str(B2)] = {"launch_us": round(t2 * 1e3, 3), "calls_per_s_per_gpu": round(B2 / (t2 * 1e-3), 1),
                                 "frac": round(B2 * flops / (t2 * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4)}
+
+            # the opt-in persistent streaming kernel (forced plan 23; mha_hd64_set_stream_mode(1))
+            def stream_launch(qs=qs, ks=ks, vs=vs, os_=os_, B2=B2):
+                st = lib.mha_hd64_launch_forced(qs.data_ptr(), ks.data_ptr(), vs.data_ptr(), os_.data_ptr(), B2, 4, nq,
+                                                nkv, 0, 0, 23, 0, 0, ws_buf2.data_ptr(), ws_buf2.numel(),
+                                                torch.cuda.current_stream(device).cuda_stream, 3)
+                assert st == 0
+            t3 = graph_per_launch_ms(torch, stream_launch, stream, k=50)
+            sweep_b[str(B2)]["stream_kernel"] = {
+                "launch_us": round(t3 * 1e3, 3),
+                "frac": round(B2 * flops / (t3 * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4)}
             del qs, ks, vs, os_
         result["batched"]["more_calls_per_launch"] = sweep_b
         # two streams of 16-call launches (two pair streams): one launch's prologue and tail overlap

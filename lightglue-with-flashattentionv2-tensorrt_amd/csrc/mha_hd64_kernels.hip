@@ -1052,19 +1052,25 @@ static bool direct16_enabled() {
 }
 
 // The persistent streaming kernel (mha_hd64_stream.hip) for launches of many 128-row blocks
-// (MHA_HD64_STREAM=0: never, 1: for every fp16 launch past one round of 16-row blocks).
-static int stream_env() {
-    static const int v = [] {
+// (MHA_HD64_STREAM=0 / set_stream_mode(0): never (default); 1: for every fp16 launch past one round
+// of 128-row blocks). Opt-in: it ties the ring kernel from 16 batched calls up and loses below
+// (DESIGN.md section 8.5).
+std::atomic<int> g_stream_mode{-1};
+int stream_env() {
+    int v = g_stream_mode.load();
+    if (v < 0) {
         const char* e = std::getenv("MHA_HD64_STREAM");
-        return e ? (e[0] == '0' ? 0 : 1) : -1;
-    }();
+        int expect = -1;
+        g_stream_mode.compare_exchange_strong(expect, (e && e[0] == '1') ? 1 : 0);
+        v = g_stream_mode.load();
+    }
     return v;
 }
-// waves per streaming workgroup (MHA_HD64_STREAM_WAVES=4 or 8; A/B switch)
+// waves per streaming workgroup (MHA_HD64_STREAM_WAVES=8: 256-row items; default 4, the faster)
 static int stream_waves() {
     static const int v = [] {
         const char* e = std::getenv("MHA_HD64_STREAM_WAVES");
-        return (e && e[0] == '4') ? 4 : 8;
+        return (e && e[0] == '8') ? 8 : 4;
     }();
     return v;
 }
@@ -1282,6 +1288,7 @@ bool f32_inkernel_enabled() {
 }  // namespace
 
 void set_f32_inkernel(int enable) { g_f32_inkernel.store(enable ? 1 : 0); }
+void set_stream_mode(int mode) { g_stream_mode.store(mode ? 1 : 0); }
 
 static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutType out, void* workspace,
                                      size_t ws_bytes, hipStream_t stream, int force_q_waves, int force_kv_waves,

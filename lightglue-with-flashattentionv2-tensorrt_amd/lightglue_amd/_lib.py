@@ -144,6 +144,7 @@ HOOKS = {
     "mha_hd64_set_stamp_buffer": ([_P], None),
     "mha_hd64_set_fused_combine": ([_I], None),
     "mha_hd64_set_f32_inkernel": ([_I], None),
+    "mha_hd64_set_stream_mode": ([_I], None),
     "mha_hd64_last_combine_form": ([], _I),
 }
 
