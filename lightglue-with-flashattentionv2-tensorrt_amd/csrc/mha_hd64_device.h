@@ -12,6 +12,7 @@ namespace mha_hd64 {
 namespace {
 typedef _Float16 f16;
 typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef f16 f16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -224,10 +225,49 @@ __device__ __forceinline__ void keep_live(const f16x8& x) { asm volatile("" ::"v
 constexpr float kMaskBias = -65504.f;  // fp16 lowest: a masked key's score, exp2 -> 0
 constexpr float kEmptyMax = -30000.f;  // tile max below this: every key of the tile was masked
 
+// Non-finite query rows. The matrix-pipe row sums multiply a partner query's fp16 P by a 0
+// selector, and 0 * NaN = NaN would poison that partner's sum. So a query whose 64 dims hold a NaN
+// or an Inf (spread over lanes l and l ^ 32 of the swapped QKᵀ layout: 4 x f16x8 each) has its Q
+// fragments zeroed (its P stays finite) and its output row written as NaN, which is what the
+// reference's math gives such a row. Returns the mask of the wave's 32 queries that are bad
+// (wave-uniform). Integer tests only: the kernels are built with -fno-honor-nans.
+__device__ __forceinline__ unsigned q_nonfinite_fix(f16x8 (&q)[4]) {
+    float s = 0.f;  // the sum of 32 finite fp16 values is finite (|s| <= 32 * 65504)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        // (h2 built element-wise: a bit_cast of a vector element w[j] here compiles to w[0] four
+        // times with this compiler)
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            s = __builtin_amdgcn_fdot2(h2{q[i][2 * j], q[i][2 * j + 1]}, h2{(_Float16)1.f, (_Float16)1.f}, s, false);
+    }
+    // the bits through an asm move: on a bit-cast float the compiler reads this test as an
+    // fp-class test and, under -fno-honor-nans, drops its NaN half
+    unsigned bits;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(bits) : "v"(s));
+    const bool bad_lane = (bits & 0x7f800000u) == 0x7f800000u;
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(bad_lane);
+    const unsigned qm = (unsigned)m | (unsigned)(m >> 32);
+    if (qm) {  // rare: zero the bad queries' fragments
+        const bool bad = (qm >> (__lane_id() & 31)) & 1u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = bad ? f16x8{} : q[i];
+    }
+    return qm;
+}
+// 1 / l, or a quiet NaN for a bad query (opaque to the -fno-honor-nans folds)
+__device__ __forceinline__ float inv_or_nan(float l, unsigned qm, int query) {
+    unsigned b = __builtin_bit_cast(unsigned, 1.f / l);
+    b = ((qm >> query) & 1u) ? 0x7fc00000u : b;
+    float r = __builtin_bit_cast(float, b);
+    asm volatile("" : "+v"(r));
+    return r;
+}
+
 // Buffer loads (T8): a per-head descriptor whose record count is the head's byte size, so
 // rows past nq / nkv read as zeros in hardware (no clamps, no 64-bit address math per load);
 // the per-iteration key offset rides in the scalar soffset.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
 }

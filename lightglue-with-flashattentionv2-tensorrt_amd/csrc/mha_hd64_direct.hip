@@ -95,7 +95,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
     // Wave-private region: the wave's V tiles, later its staged Oᵀ (8704 = 68 x 128 B keeps the
     // bank phase of every region the same as a region at 0).
     constexpr int RS = TPW * kTileBytes > EPI_WAVE ? TPW * kTileBytes : EPI_WAVE;
-    constexpr int LDS_BYTES = KW * RS + KW * BLOCK_M * 2 * 4;
+    constexpr int LDS_BYTES = KW * RS + KW * BLOCK_M * 2 * 4 + 16;  // + wave 0's non-finite-query mask
     static_assert(RS % 128 == 0 && LDS_BYTES <= 160 * 1024, "LDS layout");
     __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
     lds_char* const lds = (lds_char*)smem;
@@ -141,6 +141,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
     f32x16 o0, o1;  // Oᵀ: dims 0..31 / 32..63, query on the lane
     f32x4 l_acc;
     float m_run = 0.f;
+    unsigned qbad = 0;  // queries of the block with a non-finite Q (q_nonfinite_fix)
 
     if (n_t == 0) {  // a wave wholly past nkv contributes nothing (m = -inf in the merge)
         o0 = o1 = f32x16{};
@@ -239,6 +240,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
                 qf[s] = __builtin_bit_cast(f16x8, outv);
             }
         }
+        qbad = q_nonfinite_fix(qf);  // non-finite query rows: zeroed here, NaN rows at the store
 
         // Row sums on the matrix pipe and the bias k-step: as the ring kernel (mha_hd64_kernels.hip).
         const f16 sel = (((lane & 15) >> 2) & 1) == ((lane >> 4) & 1) ? (f16)1.f : (f16)0.f;
@@ -531,6 +533,8 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
                 f32x4{o1[4 * g4], o1[4 * g4 + 1], o1[4 * g4 + 2], o1[4 * g4 + 3]};
         }
         if (hh == 0) *reinterpret_cast<float2*>(mlb + (wave * BLOCK_M + r) * 2) = make_float2(m_w, L_w);
+        // wave 0 always holds keys, so its mask is the block's (a keyless wave loads no Q)
+        if (wave == 0 && lane == 0) *reinterpret_cast<unsigned*>(mlb + KW * BLOCK_M * 2) = qbad;
     }
     __syncthreads();
     DSTAMP(5);
@@ -560,7 +564,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct_kernel(FwdArgs a) 
     if (q < nq && !(MHA_ABL & ABL_NO_STORE)) {
         const __amdgpu_buffer_rsrc_t o_rs = make_rsrc(reinterpret_cast<TOut*>(ca.o) + (size_t)bh * nq * kHeadDim,
                                                       (unsigned)(nq * kHeadDim * sizeof(TOut)));
-        const float inv = 1.f / L;
+        const float inv = inv_or_nan(L, *reinterpret_cast<const unsigned*>(mlb + KW * BLOCK_M * 2), row);
         store_dims<TOut, DPT, MHA_ST_AUX>(o_rs, (unsigned)((q * kHeadDim + c) * sizeof(TOut)), acc0 * inv, acc1 * inv);
     }
 #ifdef MHA_STAMPS

@@ -679,6 +679,9 @@ hipError_t launch_direct16(const FwdArgs& a, int grid, int tiles_per_wave, bool 
     // tiles_per_wave counts 64-key tiles per wave of the 8-wave form (1: nkv <= 512, 2: <= 1024);
     // 4 waves take twice as many
     if (in_f32) {  // fp32 Q/K/V rounded in the kernel: the one-pass forms (the planner's choice)
+        if (tiles_per_wave > 2)  // two-pass forms: diagnostic only (MHA_HD64_F32_INKERNEL=2)
+            return out_f32 ? launch16_t<float, 4, 4, 2, true>(a, grid, stream)
+                           : launch16_t<f16, 4, 4, 2, true>(a, grid, stream);
         switch (tiles_per_wave * 2 + (out_f32 ? 1 : 0)) {
             case 2: return launch16_t<f16, 4, 2, 1, true>(a, grid, stream);
             case 3: return launch16_t<float, 4, 2, 1, true>(a, grid, stream);

@@ -189,6 +189,11 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
 #pragma unroll
             for (int e = 0; e < 8; ++e) qf[rb][s][e] = (f16)((float)h[e] * kScaleLog2);
         }
+    // queries with a non-finite Q: fragments zeroed here, their O rows poisoned to NaN before the
+    // merge (q_nonfinite_fix, mha_hd64_device.h), so every merge and combine downstream carries it
+    unsigned qbad[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) qbad[rb] = q_nonfinite_fix(qf[rb]);
 
     // Prologue: stage 0 is published first so QKᵀ(0) starts while the next stage(s) are in flight
     // (published right after it).
@@ -548,6 +553,11 @@ __global__ __launch_bounds__(64 * QW * KW, 1) void mha_hd64_fwd_kernel(FwdArgs a
     float* mlb = ol + KW * BLOCK_M * OROW;          // [KW][BLOCK_M][2]
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
+        if (qbad[rb]) {  // wave-uniform, rare
+            const float pois = inv_or_nan(1.f, qbad[rb], r);  // NaN on a bad query's lanes, else 1
+            o0[rb] *= pois;
+            o1[rb] *= pois;
+        }
         const float L_w = l_acc[rb][0];  // the row-sum MFMA already spans both half-waves
         const float m_w = (L_w > 0.f) ? m_run[rb] : -INFINITY;
         const int row = qw * 32 * RB + 32 * rb + r;
@@ -840,6 +850,7 @@ template <typename TIn, typename TOut>
 hipError_t launch_fwd_shape(const FwdArgs& a, int grid, int qw, int kw, int rb, hipStream_t stream) {
     if (a.n_calls > 1) {
         switch (rb * 64 + qw * 8 + kw) {
+            case 64 + 4 * 8 + 1: return launch_fwd<TIn, TOut, 4, 1, 1, true>(a, grid, stream);  // > 256 128-row blocks
             case 64 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 1, true>(a, grid, stream);
             case 64 + 4 * 8 + 2: return launch_fwd<TIn, TOut, 4, 2, 1, true>(a, grid, stream);
             case 128 + 2 * 8 + 2: return launch_fwd<TIn, TOut, 2, 2, 2, true>(a, grid, stream);
@@ -1280,14 +1291,17 @@ bool f32_inkernel_enabled() {
     if (v < 0) {
         const char* e = std::getenv("MHA_HD64_F32_INKERNEL");
         int expect = -1;
-        g_f32_inkernel.compare_exchange_strong(expect, (e && e[0] == '0') ? 0 : 1);
+        g_f32_inkernel.compare_exchange_strong(expect, (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1);
         v = g_f32_inkernel.load();
     }
-    return v == 1;
+    return v >= 1;
 }
+// 2 (MHA_HD64_F32_INKERNEL=2 / set_f32_inkernel(2)): the two-pass forms (1024 < nkv <= 2048) round
+// fp32 in the kernel too. Diagnostic: measured slower than convert + fp16 kernel.
+bool f32_inkernel_two_pass() { return f32_inkernel_enabled() && g_f32_inkernel.load() == 2; }
 }  // namespace
 
-void set_f32_inkernel(int enable) { g_f32_inkernel.store(enable ? 1 : 0); }
+void set_f32_inkernel(int enable) { g_f32_inkernel.store(enable <= 0 ? 0 : enable >= 2 ? 2 : 1); }
 void set_stream_mode(int mode) { g_stream_mode.store(mode ? 1 : 0); }
 
 static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutType out, void* workspace,
@@ -1345,7 +1359,8 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
             // one-pass forms only (nkv <= 1024): the two-pass form rounding fp32 in the kernel
             // measured slower than convert + fp16 kernel (1x4x1024x2048 11.32 vs 10.75 us,
             // 512x1536 9.78 vs 9.24; profiles/r02/float_inkernel.jsonl)
-            in32_direct = p16.direct_tiles > 0 && p16.direct_tiles <= 2 && p16.rows_per_wave == 16;
+            in32_direct = p16.direct_tiles > 0 && p16.direct_tiles <= (f32_inkernel_two_pass() ? 4 : 2) &&
+                          p16.rows_per_wave == 16;
             if (in32_direct) p = p16;
         }
         if (!in32_direct) {
@@ -1474,8 +1489,8 @@ hipError_t launch_group(const Call* calls, int n, InType in, OutType out, void* 
 static size_t chunk_workspace_bytes(const Call* calls, int n, InType in) {
     if (in == InType::F32 && f32_convert_enabled()) {
         const GroupPlan p16 = plan_group(calls, n, 0, 0, 0, 0, InType::F16);
-        const bool in32_direct = f32_inkernel_enabled() && p16.direct_tiles > 0 && p16.direct_tiles <= 2 &&
-                                 p16.rows_per_wave == 16;
+        const bool in32_direct = f32_inkernel_enabled() && p16.direct_tiles > 0 &&
+                                 p16.direct_tiles <= (f32_inkernel_two_pass() ? 4 : 2) && p16.rows_per_wave == 16;
         if (in32_direct) return 0;
         if (p16.direct_tiles > 0 || p16.stream) {  // convert launch into the workspace, then the fp16 kernel
             size_t off = 0;

@@ -22,10 +22,12 @@
 //    while the current item finishes. The next item's Q arrives by DMA in a 16 KiB region during
 //    the current item's first step; its first QKᵀ runs in the current item's last step. An item
 //    seam costs the output stores and a few register moves; nothing waits for a fresh burst;
-//  * per step (64 keys, one barrier): phase A = QKᵀ of the next tile (v_mfma_f32_32x32x16_f16,
-//    Sᵀ = K·Qᵀ so a lane holds one query) ‖ exp2 of this tile; phase B = Oᵀ += Vᵀ·Pᵀ of this tile
-//    (P straight from the score registers, Vᵀ by ds_read_b64_tr_b16) + row sums on the matrix pipe
-//    ‖ row max of the next tile;
+//  * per step t (64 keys, one barrier), deferred P·V: the matrix pipe runs QKᵀ of tile t+1
+//    (v_mfma_f32_32x32x16_f16, Sᵀ = K·Qᵀ so a lane holds one query) and then Oᵀ += Vᵀ·Pᵀ of tile
+//    t−1 (P packed to fp16 in the previous step, Vᵀ by ds_read_b64_tr_b16) + its row sums, while
+//    the vector pipes run exp2 and the fp16 pack of tile t and the row max of tile t+1; so no
+//    MFMA waits for the exponentials of its own step. The ring slot of every operand is a
+//    compile-time constant (the loop body is unrolled over the 4 slots);
 //  * the running max rides in the QKᵀ chains' C operand (a register block holding −m, read, never
 //    written: the MFMA emits s·c − m), so a probability is one v_exp_f32 and there is no bias
 //    k-step; lazy rescale (threshold 8, log2 units) as the other kernels;
@@ -296,9 +298,11 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) void mha_hd64_stream_kern
     };
     // Q fragments of this wave's rows from the Q region, scaled
     f16x8 qf[4];
-    auto read_q = [&]() {
+    // (returns the mask of the wave's queries with a non-finite Q, whose fragments it zeroes)
+    auto read_q = [&]() -> unsigned {
 #pragma unroll
         for (int s = 0; s < 4; ++s) qf[s] = stream_scale_q(lds_read16(lds, q_addr + k_addr[s]));
+        return q_nonfinite_fix(qf);
     };
 
     // ---- compute state ----
@@ -308,6 +312,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) void mha_hd64_stream_kern
     StreamItem nxt = stream_item<MULTI, OSZ, NW>(a, has_next ? j + G : j);
     StreamItem prv = cur;       // the item whose last PV is pending (stored after the next first step)
     bool has_prv = false;
+    unsigned qbad = 0, qbad_next = 0, qbad_prv = 0;  // non-finite query masks (current / next / previous item)
     int t = 0;                  // tile of the current item
     f32x16 cm;                  // -m (the QKᵀ chains' C operand)
     f32x16 o0 = {}, o1 = {};    // Oᵀ: dims 0..31 / 32..63, query on the lane
@@ -354,8 +359,8 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) void mha_hd64_stream_kern
         else l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, pv[jj][ss], l_acc, 0, 0, 0);
     };
     // O = Oᵀ / l of item `it` (rows past nq: dropped by the descriptor)
-    auto epilogue = [&](const StreamItem& it) {
-        const float inv = 1.f / l_acc[0];
+    auto epilogue = [&](const StreamItem& it, unsigned qbad_it) {
+        const float inv = inv_or_nan(l_acc[0], qbad_it, r);  // a non-finite query row: NaN
         const __amdgpu_buffer_rsrc_t o_rs = stream_rsrc(it.o, (unsigned)it.nq * kHeadDim * OSZ);
         const unsigned row = (unsigned)(it.q0 + 32 * wave + r);
         if constexpr (OSZ == 2) {
@@ -404,7 +409,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) void mha_hd64_stream_kern
         lds_write16(lds, (NS - 1) * kStreamSlot + kTileBytes + off, f16x8{});
     stream_wait<WAITN>();
     __builtin_amdgcn_s_barrier();
-    read_q();
+    qbad = read_q();
     {
         f16x8 kf[8];
 #pragma unroll
@@ -484,7 +489,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) void mha_hd64_stream_kern
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();
             }
-            read_q();
+            qbad_next = read_q();
             cm = f32x16{};
         }
         if (first && !seam) issue_q(nxt);  // the next item's Q: the region is free since the last seam
@@ -623,7 +628,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) void mha_hd64_stream_kern
             unsigned long long e0, e1;
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(e0)::"memory");
 #endif
-            epilogue(prv);
+            epilogue(prv, qbad_prv);
             o0 = f32x16{};
             o1 = f32x16{};
             l_acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -647,11 +652,13 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) void mha_hd64_stream_kern
                 pv_mfma(k, pn, 1);
                 pv_mfma(k, pn, 2);
             }
-            epilogue(cur);
+            epilogue(cur, qbad);
             return false;
         }
         prv = cur;
         has_prv = true;
+        qbad_prv = qbad;
+        qbad = qbad_next;
         j += G;
         cur = nxt;
         nt = (cur.nkv + kTileKV - 1) / kTileKV;

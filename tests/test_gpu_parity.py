@@ -941,3 +941,70 @@ def test_concurrency_hint_plans_match_oracle(hint, nq, nkv, dev, oracle_mod):
     assert torch.equal(a, b)
     assert _maxdiff(got, ref) <= TOL
     _regress16(got, ref)
+
+
+@pytest.mark.parametrize("in_dt,out_dt,tol", [(torch.float16, torch.float16, TOL), (torch.float16, torch.float32, TOL_F32OUT),
+                                              (torch.float32, torch.float32, TOL)])
+def test_grouped_past_one_round_of_128_row_blocks(in_dt, out_dt, tol, dev, oracle_mod):
+    """Grouped launches whose calls carry more than 256 128-row blocks and more 32-row blocks than
+    the single-pass kernels take: the planner's ring shape (4,1) in its multi-call form (a
+    regression: that form was not instantiated and the launch failed with 'invalid argument')."""
+    from lightglue_amd import _lib, mha_hd64_grouped
+
+    lib = _lib.load()
+    for shapes in ([(8, 1024, 1024), (8, 1024, 1024)], [(12, 1024, 1024), (6, 512, 700), (3, 1000, 77), (9, 200, 1500)]):
+        host = _group_inputs(shapes, 61 + len(shapes), np.float16 if in_dt == torch.float16 else np.float32)
+        dev_t = [tuple(_t(x, dev, in_dt) for x in c) for c in host]
+        outs = mha_hd64_grouped(dev_t, out_dtype=out_dt)
+        torch.cuda.synchronize()
+        for (qh, kh, vh), o in zip(host, outs):
+            b, nq = qh.shape[0], qh.shape[2]
+            rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 24)), nq - 1])
+            bsel = sorted({0, b - 1})
+            q16, k16, v16 = (np.ascontiguousarray(x[bsel]).astype(np.float16).astype(np.float32) for x in (qh, kh, vh))
+            ref = oracle_mod.attention_c(np.ascontiguousarray(q16[:, :, rows]), k16, v16)
+            got = o.float().cpu().numpy()
+            assert np.isfinite(got).all()
+            d = _maxdiff(got[bsel][:, :, rows], ref)
+            assert d <= tol, (shapes, qh.shape, d)
+
+
+# every kernel form (forced plan codes: q_waves, kv_waves, splits as mha_hd64_launch_forced)
+NONFINITE_PLANS = [(21, 0, 0), (22, 0, 0), (23, 0, 0), (4, 2, 0), (4, 1, 0), (2, 2, 2), (1, 8, 0), (12, 2, 0), (2, 4, 0)]
+
+
+@pytest.mark.parametrize("val,where", [(np.nan, "q"), (np.nan, "k"), (np.nan, "v"), (np.inf, "q"), (np.inf, "v")])
+def test_nonfinite_inputs_every_plan(val, where, dev):
+    """A NaN or Inf in one element reaches exactly the outputs it reaches in the reference's PyTorch
+    math, in every kernel form: a query row -> that row only (the matrix-pipe row sums pair each
+    query with a partner under a 0 selector, and 0 * NaN would also poison the partner: such a
+    query's Q is zeroed in the kernel and its row written as NaN, q_nonfinite_fix); a key row ->
+    every row of the head; a value element -> its output column. (An Inf in K is not covered: the
+    queries whose score goes to +Inf give NaN rows as in the reference, and their row-sum partners
+    can go NaN with them)"""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    ws = torch.empty(1 << 22, dtype=torch.uint8, device=dev)
+    for b, n in ((1, 100), (2, 300)):
+        qn, kn, vn = synth.qkv(4711 + n, n, n, batch=b)
+        x = {"q": qn, "k": kn, "v": vn}[where]
+        x[b - 1, 1, n // 3, 5] = val
+        q16, k16, v16 = (synth.round_f16(a) for a in (qn, kn, vn))
+        qf, kf, vf = (torch.from_numpy(a).double() for a in (q16, k16, v16))
+        ref = torch.softmax((qf @ kf.transpose(-1, -2)) * 0.125, -1) @ vf
+        q, k, v = (_t(a, dev, torch.float16) for a in (q16, k16, v16))
+        for code, kw, sp in NONFINITE_PLANS:
+            for out_dt in (torch.float16, torch.float32):
+                o = torch.zeros(q.shape, dtype=out_dt, device=dev)
+                st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), b, 4, n, n, 0,
+                                                int(out_dt == torch.float32), code, kw, sp, ws.data_ptr(), ws.numel(),
+                                                torch.cuda.current_stream().cuda_stream, 3)
+                if st != 0:  # a forced shape this size does not take (e.g. no split for one tile)
+                    continue
+                torch.cuda.synchronize()
+                got = o.double().cpu()
+                assert torch.equal(torch.isnan(got), torch.isnan(ref)), (where, val, b, n, code, kw, sp, out_dt)
+                fin = torch.isfinite(ref)
+                d = float((got[fin] - ref[fin]).abs().max()) if fin.any() else 0.0
+                assert d <= TOL, (where, val, b, n, code, kw, sp, out_dt, d)

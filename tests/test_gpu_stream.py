@@ -124,7 +124,10 @@ def test_stream_kernel_running_max_moves(dev, oracle_mod):
 
 def test_stream_kernel_large_negative_logits(dev, oracle_mod):
     """Scores far below zero everywhere (~ -200 raw, as test_gpu_parity.py's case) in a launch of
-    several items per workgroup: each item's first tile must set its max (no underflow to l = 0)."""
+    several items per workgroup: each item's first tile must set its max (no underflow to l = 0).
+    At this logit scale the fp16 operands of Q·Kᵀ alone put every plan ~6e-3 from the fp64 oracle
+    (tools/_extreme_logits.py: identical errors across plans 0/1/21/22/23), so both output types
+    take the 1e-2 contract here, and the stream kernel must agree with the planner's plan."""
     from lightglue_amd import _lib, synth
 
     lib = _lib.load()
@@ -136,14 +139,17 @@ def test_stream_kernel_large_negative_logits(dev, oracle_mod):
     bsel = [0, 21, batch - 1]
     ref = oracle_mod.attention_c(q16[bsel], k16[bsel], v16[bsel])
     q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
-    for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
+    for out_dt in (torch.float16, torch.float32):
         o = torch.empty(q.shape, dtype=out_dt, device=dev)
         _launch(lib, q, k, v, o)
+        o2 = torch.empty(q.shape, dtype=out_dt, device=dev)
+        _launch(lib, q, k, v, o2, code=0)
         torch.cuda.synchronize()
         got = o.float().cpu().numpy()
         assert np.isfinite(got).all()
         d = _maxdiff(got[bsel], ref)
-        assert d <= tol, (out_dt, d)
+        dp = _maxdiff(got, o2.float().cpu().numpy())
+        assert d <= TOL and dp <= 2e-3, (out_dt, d, dp)
 
 
 @pytest.mark.parametrize("out_dt,tol", [(torch.float16, TOL), (torch.float32, TOL_F32OUT)])

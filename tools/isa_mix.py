@@ -14,7 +14,7 @@ body = lines[start:end]
 blocks, cur, label = [], [], "entry"
 for l in body:
     s = l.strip()
-    if re.match(r"^\.LBB\d+_\d+:", s):
+    if re.match(r"^\.LBB\d+_\d+:", s) or re.match(r"^; %bb\.\d+:", s):
         blocks.append((label, cur))
         label, cur = s[:-1], []
         continue
