@@ -16,27 +16,35 @@ def main():
     import lightglue_amd
     from lightglue_amd import synth
 
-    shapes = [tuple(int(x) for x in s.split("-")) for s in sys.argv[1:]] or [(1024, 1024), (512, 512)]
+    # "nq-nkv" or "BxNQ-NKV" (B calls stacked in the batch dimension of one launch)
+    def parse(s):
+        b, _, rest = s.rpartition("x")
+        nq, nkv = (int(x) for x in rest.split("-"))
+        return int(b or 1), nq, nkv
+
+    shapes = [parse(s) for s in sys.argv[1:]] or [(1, 1024, 1024), (1, 512, 512)]
     dev = torch.device("cuda", 0)
     stream = torch.cuda.Stream(dev)
     barrier, reduce_max = bench.make_collectives(torch, None)
-    for nq, nkv in shapes:
-        q, k, v = (torch.from_numpy(x).to(dev).float().contiguous() for x in synth.qkv(100, nq, nkv))
+    for b, nq, nkv in shapes:
+        q, k, v = (torch.from_numpy(x).to(dev).float().contiguous() for x in synth.qkv(100, nq, nkv, batch=b))
+        call = lightglue_amd.mha_hd64 if b == 1 else lightglue_amd.mha_hd64_batched
         out = torch.empty_like(q)
         with torch.cuda.stream(stream):
             for _ in range(50):
-                lightglue_amd.mha_hd64(q, k, v, out=out)
+                call(q, k, v, out=out)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=stream):
             for _ in range(2000):
-                lightglue_amd.mha_hd64(q, k, v, out=out)
+                call(q, k, v, out=out)
         g.replay()
         stream.synchronize()
         t, _ = bench.timed_replays(torch, g.replay, stream, barrier, reduce_max, 5)
         ref = torch.softmax((q.half().float() @ k.half().float().transpose(-1, -2)) * 0.125, -1) @ v.half().float()
         print(json.dumps({"lib": os.environ.get("MHA_HD64_LIB", "default"),
-                          "inkernel": os.environ.get("MHA_HD64_F32_INKERNEL", "1"), "nq": nq, "nkv": nkv,
-                          "us_per_call": round(t / 2000 * 1e6, 3),
+                          "inkernel": os.environ.get("MHA_HD64_F32_INKERNEL", "1"),
+                          "convert": os.environ.get("MHA_HD64_F32_CONVERT", "1"), "batch": b, "nq": nq, "nkv": nkv,
+                          "us_per_launch": round(t / 2000 * 1e6, 3),
                           "max_abs_vs_fp32_of_fp16_inputs": float((out - ref).abs().max()),
                           "digest": hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest()[:16]}), flush=True)
 
