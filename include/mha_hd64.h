@@ -167,8 +167,14 @@ int32_t mha_hd64_launch_fp32in_fp32out(const void* q, const void* k, const void*
                                        void* workspace, size_t ws_bytes, hipStream_t stream);
 
 /* Workspace bytes the launchers can use to split the KV range of a call of
- * this shape across workgroups (0 = the call never splits). */
+ * this shape across workgroups (0 = the call never splits). fp16 inputs. */
 size_t mha_hd64_launch_workspace_bytes(int32_t batch, int32_t heads, int32_t nq, int32_t nkv);
+/* The same for inputs of in_type (mha_hd64_dtype_t). For FLOAT inputs that the planner runs as a
+ * convert launch + an fp16 single-pass kernel this includes the fp16 copies of Q/K/V; with less
+ * workspace mha_hd64_launch_fp32in_fp32out takes the ring kernel rounding on load instead (same
+ * results within the tolerance, up to ~1.8x slower at 1x4x1024x2048). 0 for an invalid in_type. */
+size_t mha_hd64_launch_workspace_bytes_typed(int32_t batch, int32_t heads, int32_t nq, int32_t nkv,
+                                             int32_t in_type);
 
 /* ---- grouped launcher ----
  * Several independent calls of (possibly) different shapes in one launch. A LightGlue layer

@@ -1308,13 +1308,32 @@ static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutTyp
                                      size_t ws_bytes, hipStream_t stream, int force_q_waves, int force_kv_waves,
                                      int force_splits, int phase_mask);
 
+// Whether an fp32-input launch whose fp16 plan is p16 takes the convert launch + that fp16 kernel
+// (true) or the ring kernel rounding fp32 on load (false). The 32-row single-pass kernel after a
+// convert loses to the ring kernel past one round of its blocks and at short key ranges, where
+// the ring kernel's 128-row blocks share each K/V tile over four query waves (tools/f32_routes.py,
+// profiles/r03/f32_routes.jsonl, us per launch, convert + 32-row kernel vs ring: 4x4x1024^2 16.4
+// vs 13.9, 4x4x512^2 8.7 vs 7.6; kept: 2x4x1024^2 10.4 vs 12.8, 2x4x2048^2 22.4 vs 22.1).
+static bool f32_convert_route(const Call* calls, int n, const GroupPlan& p16) {
+    if (p16.stream) return true;
+    if (p16.direct_tiles == 0) return false;
+    if (p16.rows_per_wave == 16) return true;  // the 16-row kernel's two-pass forms (nkv > 1024)
+    long blocks = 0;
+    int max_nkv = 0;
+    for (int i = 0; i < n; ++i) {
+        blocks += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 31) / 32);
+        max_nkv = std::max(max_nkv, calls[i].nkv);
+    }
+    return blocks <= 256 && max_nkv > 512;
+}
+
 // The convert + single-pass form of an fp32-input launch, or hipErrorNotSupported when it does
 // not apply (not the planner's choice, no single-pass plan for these shapes, workspace too small).
 static hipError_t launch_f32_via_f16(const Call* calls, int n, OutType out, void* workspace, size_t ws_bytes,
                                      hipStream_t stream, int phase_mask) {
     if (!f32_convert_enabled() || !workspace) return hipErrorNotSupported;
     const GroupPlan p16 = plan_group(calls, n, 0, 0, 0, 0, InType::F16);
-    if (p16.direct_tiles == 0 && !p16.stream) return hipErrorNotSupported;
+    if (!f32_convert_route(calls, n, p16)) return hipErrorNotSupported;
     Call c16[kMaxCalls];
     ConvArgs cv{};
     size_t off = 0;
@@ -1492,7 +1511,7 @@ static size_t chunk_workspace_bytes(const Call* calls, int n, InType in) {
         const bool in32_direct = f32_inkernel_enabled() && p16.direct_tiles > 0 &&
                                  p16.direct_tiles <= (f32_inkernel_two_pass() ? 4 : 2) && p16.rows_per_wave == 16;
         if (in32_direct) return 0;
-        if (p16.direct_tiles > 0 || p16.stream) {  // convert launch into the workspace, then the fp16 kernel
+        if (f32_convert_route(calls, n, p16)) {  // convert launch into the workspace, then the fp16 kernel
             size_t off = 0;
             for (int i = 0; i < n; ++i) {
                 if (calls[i].nq <= 0 || calls[i].batch <= 0 || calls[i].heads <= 0) continue;

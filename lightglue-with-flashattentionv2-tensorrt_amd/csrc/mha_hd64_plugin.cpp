@@ -313,6 +313,14 @@ size_t mha_hd64_launch_workspace_bytes(int32_t batch, int32_t heads, int32_t nq,
     return mha_hd64::plan_call(c, (size_t)-1).ws_needed;
 }
 
+size_t mha_hd64_launch_workspace_bytes_typed(int32_t batch, int32_t heads, int32_t nq, int32_t nkv, int32_t in_type) {
+    if (in_type != MHA_HD64_DT_HALF && in_type != MHA_HD64_DT_FLOAT) return 0;
+    if (batch <= 0 || heads <= 0 || nq <= 0 || nkv <= 0) return 0;
+    const mha_hd64::Call c{nullptr, nullptr, nullptr, nullptr, batch, heads, nq, nkv};
+    return mha_hd64::group_workspace_bytes(&c, 1, in_type == MHA_HD64_DT_FLOAT ? mha_hd64::InType::F32
+                                                                              : mha_hd64::InType::F16);
+}
+
 // ---- grouped launcher ----
 static int32_t to_calls(const mha_hd64_call_t* calls, int32_t n, std::vector<mha_hd64::Call>& out) {
     MHA_CHECK(n >= 0 && (n == 0 || calls != nullptr));

@@ -113,6 +113,7 @@ SIGNATURES = {
     "mha_hd64_launch_fp16in_fp32out": ([_P, _P, _P, _P, _I, _I, _I, _I, _P, _S, _P], _I),
     "mha_hd64_launch_fp32in_fp32out": ([_P, _P, _P, _P, _I, _I, _I, _I, _P, _S, _P], _I),
     "mha_hd64_launch_workspace_bytes": ([_I, _I, _I, _I], _S),
+    "mha_hd64_launch_workspace_bytes_typed": ([_I, _I, _I, _I, _I], _S),
     "mha_hd64_launch_grouped": ([ctypes.POINTER(CallDesc), _I, _I, _I, _P, _S, _P], _I),
     "mha_hd64_grouped_workspace_bytes": ([ctypes.POINTER(CallDesc), _I], _S),
     "mha_hd64_grouped_workspace_bytes_typed": ([ctypes.POINTER(CallDesc), _I, _I], _S),

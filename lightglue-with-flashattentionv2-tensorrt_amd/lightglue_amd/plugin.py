@@ -287,7 +287,8 @@ def mha_hd64_batched(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor
         out = torch.empty(query.shape, dtype=out_dtype, device=query.device)
     lib = _lib.load()
     stream = torch.cuda.current_stream(query.device).cuda_stream
-    nbytes = lib.mha_hd64_launch_workspace_bytes(b, h, nq, nkv)
+    # (fp32 inputs: room for the fp16 copies when the planner converts before a single-pass kernel)
+    nbytes = lib.mha_hd64_launch_workspace_bytes_typed(b, h, nq, nkv, _DT[query.dtype])
     ws = _workspace(query.device, stream, nbytes) if nbytes else None
     status = getattr(lib, fn_name)(query.data_ptr(), key.data_ptr(), value.data_ptr(), out.data_ptr(), b, h, nq,
                                    nkv, ws.data_ptr() if ws is not None else None, nbytes, stream)

@@ -290,3 +290,19 @@ def test_cpu_tensors_fail_loudly():
         mha_hd64(q, q, q)
     with pytest.raises(PluginError, match="GPU"):
         mha_hd64_batched(q, q, q)
+
+
+def test_typed_launch_workspace_query(lib):
+    """mha_hd64_launch_workspace_bytes_typed: HALF equals the untyped query; FLOAT includes the
+    fp16 copies exactly where the planner converts before a single-pass kernel (1x4x1024x2048:
+    Q + K + V in fp16), nothing for the in-kernel one-pass form (1x4x1024^2) or the ring
+    kernel's convert-on-load (4x4x1024^2, past one round of 32-row blocks); 0 for bad types."""
+    HALF, FLOAT = 1, 0
+    for shape in ((1, 4, 1024, 1024), (1, 4, 1024, 2048), (2, 4, 512, 512), (4, 4, 1024, 1024), (1, 4, 33, 65)):
+        assert lib.mha_hd64_launch_workspace_bytes_typed(*shape, HALF) == lib.mha_hd64_launch_workspace_bytes(*shape)
+    assert lib.mha_hd64_launch_workspace_bytes_typed(1, 4, 1024, 1024, FLOAT) == 0
+    assert lib.mha_hd64_launch_workspace_bytes_typed(1, 4, 1024, 2048, FLOAT) == 4 * (1024 + 2 * 2048) * 64 * 2
+    assert lib.mha_hd64_launch_workspace_bytes_typed(4, 4, 1024, 1024, FLOAT) == \
+        lib.mha_hd64_launch_workspace_bytes(4, 4, 1024, 1024)
+    assert lib.mha_hd64_launch_workspace_bytes_typed(1, 4, 1024, 1024, 7) == 0
+    assert lib.mha_hd64_launch_workspace_bytes_typed(0, 4, 1024, 1024, FLOAT) == 0
