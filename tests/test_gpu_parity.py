@@ -1008,3 +1008,26 @@ def test_nonfinite_inputs_every_plan(val, where, dev):
                 fin = torch.isfinite(ref)
                 d = float((got[fin] - ref[fin]).abs().max()) if fin.any() else 0.0
                 assert d <= TOL, (where, val, b, n, code, kw, sp, out_dt, d)
+
+
+@pytest.mark.parametrize("batch,nq,nkv", [(2, 1024, 1024), (4, 1024, 1024), (4, 512, 512), (1, 1024, 2048), (3, 1000, 777)])
+def test_float_routes_batched_equals_grouped(batch, nq, nkv, dev, oracle_mod):
+    """fp32 inputs past the 16-row one-pass forms: the batched launcher sizes its workspace per
+    input type (mha_hd64_launch_workspace_bytes_typed), so it takes the same route as the grouped
+    launcher (convert + single-pass kernel, or the ring kernel rounding on load past one round of
+    32-row blocks / at nkv <= 512): bitwise-equal outputs, within the contract of the oracle on
+    the fp16-rounded inputs."""
+    from lightglue_amd import mha_hd64_batched, mha_hd64_grouped
+
+    (c,) = _group_inputs([(batch, nq, nkv)], 71 + batch, np.float32)
+    q, k, v = (_t(x, dev, torch.float32) for x in c)
+    a = mha_hd64_batched(q, k, v)
+    (b,) = mha_hd64_grouped([(q, k, v)])
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 24)), nq - 1])
+    q16, k16, v16 = (x[[0, batch - 1]].astype(np.float16).astype(np.float32) for x in c)
+    ref = oracle_mod.attention_c(np.ascontiguousarray(q16[:, :, rows]), np.ascontiguousarray(k16),
+                                 np.ascontiguousarray(v16))
+    d = _maxdiff(a.cpu().numpy()[[0, batch - 1]][:, :, rows], ref)
+    assert d <= TOL_F32OUT, d
