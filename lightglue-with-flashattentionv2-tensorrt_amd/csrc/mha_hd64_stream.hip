@@ -217,7 +217,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 1 : 2) void mha_hd64_stream_kern
     if constexpr (NW == 8) {
         if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // (wave is readfirstlane'd: a scalar branch)
     } else {
-        if (__builtin_amdgcn_readfirstlane(blockIdx.x) & 1) __builtin_amdgcn_s_setprio(1);
+        // 1: odd workgroups; 2: the second half of the grid (the second workgroup dispatched to a CU)
+        if (MHA_STREAM_PRIO == 1 ? (__builtin_amdgcn_readfirstlane(blockIdx.x) & 1)
+                                 : (__builtin_amdgcn_readfirstlane(blockIdx.x) >= gridDim.x / 2))
+            __builtin_amdgcn_s_setprio(1);
     }
 #endif
 

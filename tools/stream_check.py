@@ -121,10 +121,12 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--lib", default=_lib.LIB_PATH)
     ap.add_argument("--no-timing", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     lib = load(args.lib)
-    parity(lib, dev, args.quick)
+    if not args.no_parity:
+        parity(lib, dev, args.quick)
     if not args.no_timing:
         timing(lib, dev, args.quick)
 
