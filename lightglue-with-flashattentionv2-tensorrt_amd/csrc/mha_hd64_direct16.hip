@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "mha_hd64_device.h"
 #include "mha_hd64_internal.h"
@@ -105,6 +106,13 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
     static_assert(TPW >= 2 && TPW <= 4 && (KW == 4 || KW == 8), "waves x tiles per wave");
     static_assert(PASSES == 1 || (PASSES == 2 && TPW == 4 && KW == 4), "two passes: 4 waves x 2 x 4 tiles");
     static_assert(!F32IN || KW == 4, "fp32 inputs: the 4-wave forms");
+#ifndef MHA_D16_STAGE16
+#define MHA_D16_STAGE16 0  // A/B hook: fp16 K/V through VGPRs + ds_write (the F32IN pipeline) instead of LDS-DMA
+#endif
+    // the VGPR-staged pipeline: fp32 inputs always; fp16 inputs under the A/B hook (4-wave forms)
+    constexpr bool STAGED = F32IN || (MHA_D16_STAGE16 && KW == 4);
+    using TIn = std::conditional_t<F32IN, float, f16>;
+    constexpr unsigned ISZ = sizeof(TIn);
     constexpr int BLOCK_M = 16;                     // query rows per workgroup
     constexpr int WAVE_KEYS = kTileKV * TPW * PASSES;
     constexpr int OROW = 68;                        // epilogue fp32 row pitch
@@ -171,7 +179,7 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
 #pragma unroll
         for (int db = 0; db < 4; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
         l_acc = f32x4{0.f, 0.f, 0.f, 0.f};
-    } else if constexpr (F32IN) {
+    } else if constexpr (STAGED) {
         // ---- the Float boundary inside the kernel: fp32 Q/K/V through VGPRs ----
         // fp32 rows are 256 B. Lane L of piece i (rows 8i..8i+7 of a tile) loads the 8 floats of
         // chunk c = L & 7 of row 8i + L/8, rounds them to fp16 (RNE, as the reference's convert
@@ -179,14 +187,14 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         // it (the same images as the DMA path). Tiles in the order K(0..TPW-1), V(0..TPW-1), two
         // in flight; tile j goes into slot j % TPW once that slot's K fragments are in registers.
         // Loads are plain (compiler-tracked) buffer loads: no hand-counted waits in this form.
-        const float* Qf = reinterpret_cast<const float*>(ca.q) + (size_t)bh * nq * kHeadDim;
-        const float* Kf = reinterpret_cast<const float*>(ca.k) + (size_t)bh * nkv * kHeadDim;
-        const float* Vf = reinterpret_cast<const float*>(ca.v) + (size_t)bh * nkv * kHeadDim;
-        const __amdgpu_buffer_rsrc_t q32 = make_rsrc(Qf, (unsigned)nq * kHeadDim * 4);
-        const __amdgpu_buffer_rsrc_t k32 = make_rsrc(Kf, (unsigned)nkv * kHeadDim * 4);
-        const __amdgpu_buffer_rsrc_t v32 = make_rsrc(Vf, (unsigned)nkv * kHeadDim * 4);
+        const TIn* Qf = reinterpret_cast<const TIn*>(ca.q) + (size_t)bh * nq * kHeadDim;
+        const TIn* Kf = reinterpret_cast<const TIn*>(ca.k) + (size_t)bh * nkv * kHeadDim;
+        const TIn* Vf = reinterpret_cast<const TIn*>(ca.v) + (size_t)bh * nkv * kHeadDim;
+        const __amdgpu_buffer_rsrc_t q32 = make_rsrc(Qf, (unsigned)nq * kHeadDim * ISZ);
+        const __amdgpu_buffer_rsrc_t k32 = make_rsrc(Kf, (unsigned)nkv * kHeadDim * ISZ);
+        const __amdgpu_buffer_rsrc_t v32 = make_rsrc(Vf, (unsigned)nkv * kHeadDim * ISZ);
         struct Tile {
-            Raw8<float> p[8];
+            Raw8<TIn> p[8];
         };
         const int prow = lane >> 3, pc = lane & 7;
         // item j of the order K(0..TPW-1), V(0..TPW-1) of pass 0, then the same for pass 1:
@@ -194,9 +202,9 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         constexpr int NI = 2 * TPW * PASSES;
         auto ld_tile = [&](int j, Tile& x) {
             const int r = j % (2 * TPW), t = (j / (2 * TPW)) * TPW + r % TPW;
-            const unsigned base = ((unsigned)(key0 + kTileKV * t + prow) * kHeadDim + 8 * pc) * 4;
+            const unsigned base = ((unsigned)(key0 + kTileKV * t + prow) * kHeadDim + 8 * pc) * ISZ;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) bload8(x.p[i], r < TPW ? k32 : v32, base + i * 8 * kHeadDim * 4, 0);
+            for (int i = 0; i < 8; ++i) bload8(x.p[i], r < TPW ? k32 : v32, base + i * 8 * kHeadDim * ISZ, 0);
         };
         auto st_tile = [&](int j, const Tile& x) {
             const int r = j % (2 * TPW);
@@ -211,9 +219,9 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
         // Q: Q[q_row][32s+8g..+7] rounded to fp16, then scaled as the fp16 path does
         f16x8 qf[2];
         {
-            Raw8<float> qr[2];
+            Raw8<TIn> qr[2];
 #pragma unroll
-            for (int s = 0; s < 2; ++s) bload8(qr[s], q32, (unsigned)(q_row * kHeadDim + 32 * s + 8 * g) * 4, 0);
+            for (int s = 0; s < 2; ++s) bload8(qr[s], q32, (unsigned)(q_row * kHeadDim + 32 * s + 8 * g) * ISZ, 0);
             const float sc = kScaleLog2;
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
@@ -302,7 +310,10 @@ __global__ __launch_bounds__(64 * KW, 1) void mha_hd64_direct16_kernel(const voi
 #endif
         // 3 for the 2-tile form (1x4x512^2 5.00 vs 5.10 us), 2 for the 4-tile form (the third
         // buffer lands in AGPRs: 1024^2 7.45-7.51 vs 7.11; tools/f32_probe.py over MHA_F32_NB builds)
-        constexpr int NB = MHA_F32_NB > 0 ? MHA_F32_NB : (TPW == 2 ? 3 : 2);
+#ifndef MHA_D16_NB16
+#define MHA_D16_NB16 3  // fp16 tiles in flight per wave in the staged A/B form
+#endif
+        constexpr int NB = !F32IN ? MHA_D16_NB16 : MHA_F32_NB > 0 ? MHA_F32_NB : (TPW == 2 ? 3 : 2);
         Tile buf[NB];
 #pragma unroll
         for (int j = 0; j < NB; ++j) ld_tile(j, buf[j]);
