@@ -6,6 +6,7 @@ import os
 import re
 import subprocess
 
+import numpy as np
 import pytest
 
 from conftest import REPO
@@ -306,3 +307,29 @@ def test_typed_launch_workspace_query(lib):
         lib.mha_hd64_launch_workspace_bytes(4, 4, 1024, 1024)
     assert lib.mha_hd64_launch_workspace_bytes_typed(1, 4, 1024, 1024, 7) == 0
     assert lib.mha_hd64_launch_workspace_bytes_typed(0, 4, 1024, 1024, FLOAT) == 0
+
+
+def test_planner_invariants_fuzzed(lib):
+    """Host-only property test of the planner (no GPU): for seeded random shapes (batch 1-64,
+    heads 1-8, nq/nkv 1-4096) and workspace sizes, the plan code is one the launchers compile,
+    the split count is 1..16 with tiles_per_split covering every key tile, the workspace the plan
+    asks for fits the workspace given, and the typed queries are consistent (HALF = untyped,
+    FLOAT >= 0, both 0 only for empty shapes)."""
+    rng = np.random.default_rng(77)
+    out = (ctypes.c_int32 * 4)()
+    codes = {1, 2, 4, 12, 21, 22, 23}
+    for _ in range(400):
+        b, h = int(rng.integers(1, 65)), int(rng.integers(1, 9))
+        nq, nkv = int(rng.integers(1, 4097)), int(rng.integers(1, 4097))
+        ws = int(rng.choice([0, 1 << 16, 1 << 20, 5242880, 1 << 30]))
+        need = lib.mha_hd64_plan(b, h, nq, nkv, ws, out)
+        qw, kw, splits, tps = list(out)
+        assert qw in codes, (b, h, nq, nkv, ws, qw)
+        assert 1 <= splits <= 16 and tps >= 1, (b, h, nq, nkv, ws, splits, tps)
+        if qw not in (21, 22, 23):
+            super_tiles = -(-nkv // (64 * kw))
+            assert splits * tps >= super_tiles, (b, h, nq, nkv, ws, kw, splits, tps)
+        assert need <= ws or splits == 1, (b, h, nq, nkv, ws, need)
+        half = lib.mha_hd64_launch_workspace_bytes_typed(b, h, nq, nkv, 1)
+        assert half == lib.mha_hd64_launch_workspace_bytes(b, h, nq, nkv)
+        assert lib.mha_hd64_launch_workspace_bytes_typed(b, h, nq, nkv, 0) >= 0

@@ -1031,3 +1031,55 @@ def test_float_routes_batched_equals_grouped(batch, nq, nkv, dev, oracle_mod):
                                  np.ascontiguousarray(v16))
     d = _maxdiff(a.cpu().numpy()[[0, batch - 1]][:, :, rows], ref)
     assert d <= TOL_F32OUT, d
+
+
+@pytest.mark.parametrize("mode", ["default", "hint3", "stream"])
+def test_grouped_random_groups(mode, dev, oracle_mod):
+    """Seeded random groups through mha_hd64_grouped: 1-6 calls (chunked past 4), batch 1-12,
+    nq/nkv 1-2048, fp16 or fp32 inputs, fp16 or fp32 outputs, under the default planner, the
+    concurrency hint 3 and stream mode 1 -- every launch form the planner can pick for a group
+    (single-pass 16/32-row, their multi-round forms, the ring kernel with or without a split, the
+    convert route, the streaming kernel). NaN-filled outputs must be fully written; sampled rows of
+    the first and last batch entry against the C oracle on the fp16-rounded inputs."""
+    import lightglue_amd
+    from lightglue_amd import _lib, mha_hd64_grouped, synth
+
+    lib = _lib.load()
+    rng = np.random.default_rng({"default": 31, "hint3": 32, "stream": 33}[mode])
+    prev_hint = lightglue_amd.set_concurrency_hint(3) if mode == "hint3" else None
+    if mode == "stream":
+        lib.mha_hd64_set_stream_mode(1)
+    try:
+        for case in range(10):
+            n_calls = int(rng.integers(1, 7))
+            in_dt = torch.float32 if rng.random() < 0.3 else torch.float16
+            out_dt = torch.float32 if rng.random() < 0.5 else torch.float16
+            host, dev_calls, outs = [], [], []
+            for i in range(n_calls):
+                b = int(rng.integers(1, 13)) if rng.random() < 0.5 else 1
+                nq, nkv = int(rng.integers(1, 2049)), int(rng.integers(1, 2049))
+                qn, kn, vn = synth.qkv(3100 + 97 * case + 13 * i, nq, nkv, batch=b)
+                if in_dt == torch.float16:
+                    qn, kn, vn = (synth.round_f16(x) for x in (qn, kn, vn))
+                host.append((qn, kn, vn))
+                dev_calls.append(tuple(_t(x, dev, in_dt) for x in (qn, kn, vn)))
+                outs.append(torch.full((b, 4, nq, 64), float("nan"), dtype=out_dt, device=dev))
+            mha_hd64_grouped(dev_calls, out_dtype=out_dt, outs=outs)
+            torch.cuda.synchronize()
+            tol = TOL if (out_dt == torch.float16 or in_dt == torch.float32) else TOL_F32OUT
+            for (qn, kn, vn), o in zip(host, outs):
+                b, nq = qn.shape[0], qn.shape[2]
+                got = o.float().cpu().numpy()
+                assert np.isfinite(got).all(), (mode, case, qn.shape, kn.shape, in_dt, out_dt)
+                rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 16)), nq - 1])
+                bsel = sorted({0, b - 1})
+                q16, k16, v16 = (np.ascontiguousarray(x[bsel]).astype(np.float16).astype(np.float32)
+                                 for x in (qn, kn, vn))
+                ref = oracle_mod.attention_c(np.ascontiguousarray(q16[:, :, rows]), k16, v16)
+                d = _maxdiff(got[bsel][:, :, rows], ref)
+                assert d <= tol, (mode, case, qn.shape, kn.shape, in_dt, out_dt, d)
+    finally:
+        if prev_hint is not None:
+            lightglue_amd.set_concurrency_hint(prev_hint)
+        if mode == "stream":
+            lib.mha_hd64_set_stream_mode(0)
