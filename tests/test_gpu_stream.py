@@ -266,3 +266,33 @@ def test_stream_plan_reported_and_fp32_inputs_fall_back(dev, stream_mode):
     b = mha_hd64_batched(q.repeat(8, 1, 1, 1), k.repeat(8, 1, 1, 1), v.repeat(8, 1, 1, 1), out_dtype=torch.float32)
     torch.cuda.synchronize()
     assert torch.equal(a, b)  # fp32 inputs never take the streaming kernel
+
+
+def test_stream_mode_grouped_with_one_tile_calls(dev, oracle_mod, stream_mode):
+    """Grouped MULTI launch mixing long items with one-tile items (nkv <= 64: the next item's Q
+    is fetched and waited for inside the seam step) and a one-key call, both output types."""
+    from lightglue_amd import _lib, mha_hd64_grouped, synth
+
+    lib = _lib.load()
+    stream_mode(1)
+    shapes = [(12, 1024, 1024), (8, 300, 50), (6, 128, 1), (10, 640, 64)]
+    host = []
+    for i, (b, nq, nkv) in enumerate(shapes):
+        qn, kn, vn = synth.qkv(6200 + 11 * i, nq, nkv, batch=b)
+        host.append(tuple(synth.round_f16(x) for x in (qn, kn, vn)))
+    dev_t = [tuple(_t(x, dev, torch.float16) for x in c) for c in host]
+    plan = (ctypes.c_int32 * 4)()
+    lib.mha_hd64_plan(12, 4, 1024, 1024, 5242880, plan)
+    assert plan[0] == STREAM
+    for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
+        outs = [torch.full(q.shape, float("nan"), dtype=out_dt, device=dev) for q, _, _ in dev_t]
+        mha_hd64_grouped(dev_t, out_dtype=out_dt, outs=outs)
+        torch.cuda.synchronize()
+        for (q16, k16, v16), o in zip(host, outs):
+            got = o.float().cpu().numpy()
+            assert np.isfinite(got).all()
+            rows = _rows(q16.shape[2], 24)
+            bsel = sorted({0, q16.shape[0] - 1})
+            ref = _oracle_rows(oracle_mod, q16[bsel], k16[bsel], v16[bsel], rows)
+            d = _maxdiff(got[bsel][:, :, rows], ref)
+            assert d <= tol, (q16.shape, k16.shape, out_dt, d)
