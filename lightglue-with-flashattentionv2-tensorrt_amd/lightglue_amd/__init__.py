@@ -13,6 +13,7 @@ from .plugin import (  # noqa: F401
     mha_hd64_batched,
     mha_hd64_grouped,
     set_concurrency_hint,
+    set_stream_mode,
 )
 from . import ops  # noqa: F401,E402  (registers torch.ops.lightglue_amd.*)
 
@@ -26,6 +27,7 @@ __all__ = [
     "mha_hd64_batched",
     "mha_hd64_grouped",
     "set_concurrency_hint",
+    "set_stream_mode",
     "load_library",
     "LIB_PATH",
 ]

@@ -233,6 +233,15 @@ def set_concurrency_hint(streams: int) -> int:
     return int(_lib.load().mha_hd64_set_concurrency_hint(int(streams)))
 
 
+def set_stream_mode(mode: int) -> None:
+    """1: fp16 launches of more than 256 128-row blocks (batched image-pair streams, large grouped
+    layers) run the persistent streaming kernel (csrc/mha_hd64_stream.hip); 0 (default): the
+    planner's other plans. Same results within the contract; measured a tie with the LDS-ring
+    kernel at 16-32 calls per launch. Process-wide (MHA_HD64_STREAM=1 sets
+    1 at first use)."""
+    _lib.load().mha_hd64_set_stream_mode(int(mode))
+
+
 def _require_gpu(*ts: torch.Tensor) -> None:
     for t in ts:
         if not t.is_cuda:

@@ -32,11 +32,10 @@ def dev():
 
 @pytest.fixture
 def stream_mode(dev):
-    from lightglue_amd import _lib
+    import lightglue_amd
 
-    lib = _lib.load()
-    yield lib.mha_hd64_set_stream_mode
-    lib.mha_hd64_set_stream_mode(0)
+    yield lightglue_amd.set_stream_mode
+    lightglue_amd.set_stream_mode(0)
 
 
 def _t(x, dev, dtype):
