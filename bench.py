@@ -536,8 +536,11 @@ def cold_inputs(torch, lightglue_amd, stream, q, k, v, barrier, reduce_max, ws, 
     return {"calls_per_graph": sets, "pool_mib": round(sets * per_set / 2**20, 1),
             "calls_per_s": round(sets * ws / elapsed, 1), "us_per_call": round(elapsed / sets * 1e6, 3),
             "outputs_identical_to_each_other": ok,
-            "how": "each call on its own copy of the headline's Q/K/V (pool larger than MALL + L2), one graph of "
-                   "all calls, median of 5 replays"}
+            "how": ("each call on its own copy of the headline's Q/K/V (pool larger than MALL + L2), one graph of "
+                    "all calls, median of 5 replays") if pool_mib > 300 else
+                   ("each call on its own copy of the headline's Q/K/V from a pool larger than the eight 4 MiB L2s "
+                    "but inside the 256 MiB MALL (Infinity Cache): inputs from the MALL, as in the matcher, whose "
+                    "Q/K/V are the projection kernel's fresh outputs; one graph of all calls, median of 5 replays")}
 
 
 def sweep(torch, lib, device, stream, nq, nkv):
@@ -945,6 +948,8 @@ def main():
         }
         result["isolated_call_us"] = round(t_call * 1e3, 3)
         result["cold_inputs"] = cold_inputs(torch, lightglue_amd, stream, q, k, v, barrier, reduce_max, ws)
+        result["mall_inputs"] = cold_inputs(torch, lightglue_amd, stream, q, k, v, barrier, reduce_max, ws,
+                                            pool_mib=96)
 
         # Batched launch: `batched` independent calls stacked in the batch dimension of one launch.
         B = args.batched
