@@ -1083,3 +1083,34 @@ def test_grouped_random_groups(mode, dev, oracle_mod):
             lightglue_amd.set_concurrency_hint(prev_hint)
         if mode == "stream":
             lib.mha_hd64_set_stream_mode(0)
+
+
+@pytest.mark.parametrize("heads", [1, 2, 3, 8])
+def test_batched_launcher_other_head_counts(heads, dev, oracle_mod):
+    """The L0 launchers accept any heads (the plugin fixes H = 4): heads 1/2/3/8 at shapes that
+    put the planner on each kernel form (16-row single pass, 32-row, ring with and without a
+    split, the streaming kernel under stream mode), both output types, against the C oracle."""
+    import lightglue_amd
+    from lightglue_amd import mha_hd64_batched, synth
+
+    shapes = [(1, 1024, 1024), (2, 1000, 777), (1, 100, 2048), (12, 1024, 1024), (1, 33, 65)]
+    for mode in (0, 1):
+        lightglue_amd.set_stream_mode(mode)
+        try:
+            for i, (b, nq, nkv) in enumerate(shapes):
+                qn, kn, vn = synth.qkv(7100 + 31 * i + heads, nq, nkv, batch=b, heads=heads)
+                q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
+                q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+                rows = np.unique(np.r_[np.arange(0, nq, max(1, nq // 16)), nq - 1])
+                bsel = sorted({0, b - 1})
+                ref = oracle_mod.attention_c(np.ascontiguousarray(q16[bsel][:, :, rows]),
+                                             np.ascontiguousarray(k16[bsel]), np.ascontiguousarray(v16[bsel]))
+                for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
+                    o = mha_hd64_batched(q, k, v, out_dtype=out_dt)
+                    torch.cuda.synchronize()
+                    got = o.float().cpu().numpy()
+                    assert np.isfinite(got).all(), (heads, b, nq, nkv, mode)
+                    d = _maxdiff(got[bsel][:, :, rows], ref)
+                    assert d <= tol, (heads, b, nq, nkv, mode, out_dt, d)
+        finally:
+            lightglue_amd.set_stream_mode(0)
