@@ -8,10 +8,12 @@
 //   hipcc --offload-arch=gfx950 -O3 tools/mb_mfma_shape.hip -o tools/mb_mfma_shape && tools/mb_mfma_shape
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int ITER = 4096;
 
@@ -34,7 +36,11 @@ __global__ __launch_bounds__(256) void kern(const float* in, float* out, unsigne
     for (int it = 0; it < ITER; ++it) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-            if (SHAPE == 32) {
+            if (SHAPE == 8) {  // v_mfma_f32_32x32x8_f16: half the K of the 32x32x16 form (FLOPs counted as such)
+                const f16x4 a4 = {a[0], a[1], a[2], a[3]}, b4 = {b[0], b[1], b[2], b[3]};
+                if (g & 1) c1 = __builtin_amdgcn_mfma_f32_32x32x8f16(a4, b4, c1, 0, 0, 0);
+                else c0 = __builtin_amdgcn_mfma_f32_32x32x8f16(a4, b4, c0, 0, 0, 0);
+            } else if (SHAPE == 32) {
                 if (g & 1) c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c1, 0, 0, 0);
                 else c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c0, 0, 0, 0);
             } else {
@@ -93,7 +99,7 @@ void run(const char* name, float* in, float* out, unsigned long long* clk, int g
     }
     const double ghz = cyc / (rt / 100e6) / 1e9;
     // FLOPs: per wave per group 32x32x16 x 2 (or 2 x 16x16x32 x 2) = 32768 MACs x 2
-    const double flops = 2.0 * 32 * 32 * 16 * 4.0 * ITER * 4.0 * grid;  // 4 groups, 4 waves/WG
+    const double flops = 2.0 * 32 * 32 * (SHAPE == 8 ? 8 : 16) * 4.0 * ITER * 4.0 * grid;  // 4 groups, 4 waves/WG
     const double t = ms * 1e-3 / reps;
     printf("%-28s grid %4d: %8.1f us/launch  %7.1f TFLOP/s  in-kernel clock %.2f GHz\n", name, grid, t * 1e6,
            flops / t / 1e12, ghz);
@@ -112,6 +118,13 @@ int main() {
         h[i] = ((s >> 8) & 0xffff) / 65536.0f * 2.0f - 1.0f;
     }
     hipMemcpy(in, h, sizeof(h), hipMemcpyHostToDevice);
+    if (getenv("MB_SHAPE8")) {  // cycles of the 32x32x8 form vs 32x32x16 (us per launch, same MFMA count)
+        for (int rep = 0; rep < 2; ++rep) {
+            run<32, 0>("32x32x16, MFMA only", in, out, clk, 512);
+            run<8, 0>("32x32x8, MFMA only", in, out, clk, 512);
+        }
+        return 0;
+    }
     for (int rep = 0; rep < 2; ++rep) {
         run<32, 0>("32x32x16, MFMA only", in, out, clk, 512);
         run<16, 0>("16x16x32, MFMA only", in, out, clk, 512);
