@@ -219,10 +219,44 @@ size_t mha_hd64_grouped_workspace_bytes_typed(const mha_hd64_call_t* calls, int3
  * (each mode is deterministic). Returns the previous hint; values < 1 read as 1. Process-wide. */
 int32_t mha_hd64_set_concurrency_hint(int32_t streams);
 
+/* ---- kernel-form switches (no reference counterpart; process-wide, thread-safe, take effect at
+ * the next launch; every setting gives results within the same tolerance of the oracle) ---- */
+/* Throughput kernel for launches that carry more than one round of 128-row query blocks (batched
+ * image-pair streams, grouped layers of several pairs): 1 = the persistent streaming kernel
+ * (fp16 inputs; the planner default where it measured faster),
+ * 0 = the LDS-ring kernel. The environment variable MHA_HD64_STREAM=0/1 sets the initial value. */
+void mha_hd64_set_stream_mode(int32_t mode);
+/* FLOAT (fp32) inputs: 1 (default) = rounded to fp16 inside the attention kernel where that
+ * measured faster (one launch), 0 = always a convert launch into the workspace + the fp16 kernel,
+ * 2 = also the two-pass in-kernel forms (1024 < nkv <= 2048; diagnostic, measured slower).
+ * Outputs are bitwise identical in every mode. Env MHA_HD64_F32_INKERNEL sets the initial value. */
+void mha_hd64_set_f32_inkernel(int32_t mode);
+/* Calls whose keys are split across workgroups: 1 (default) = merged inside the launch through
+ * library-owned arrival tickets, 0 = a second (combine) kernel. Bitwise-identical results. */
+void mha_hd64_set_fused_combine(int32_t enable);
+
 /* ---- diagnostics ---- */
 const char* mha_hd64_last_error(void);           /* thread-local message of the last failure   */
 void        mha_hd64_set_abort_on_error(int32_t enable); /* 1 = abort() like PLUGIN_ASSERT     */
 const char* mha_hd64_build_info(void);           /* target arch, compiler, kernel variants      */
+
+/* ---- test and benchmark hooks (exported for tests/, tools/ and bench.py; not needed by a
+ * plugin host, no stability promise) ---- */
+/* Launch with a forced kernel form: q_waves/kv_waves/splits as the planner's fields (0 = the
+ * planner's choice); q_waves 21 / 22 / 23 force the 32-row / 16-row single-pass kernel / the
+ * streaming kernel. phase_mask: 1 main kernel only, 2 combine only, 3 both. Returns a status
+ * (BAD_PARAM when the form is not compiled for the shape). */
+int32_t mha_hd64_launch_forced(const void* q, const void* k, const void* v, void* o, int32_t batch, int32_t heads,
+                               int32_t nq, int32_t nkv, int32_t in_f32, int32_t out_f32, int32_t q_waves,
+                               int32_t kv_waves, int32_t splits, void* workspace, size_t ws_bytes,
+                               hipStream_t stream, int32_t phase_mask);
+/* The planner's choice for a fp16 call: out4 = {q_waves (or 21/22/23), kv_waves, splits,
+ * tiles_per_split}; returns the workspace bytes that plan uses. */
+size_t mha_hd64_plan(int32_t batch, int32_t heads, int32_t nq, int32_t nkv, size_t ws_bytes, int32_t* out4);
+/* Per-workgroup timestamp buffer of -DMHA_STAMPS diagnostic builds (ignored by release builds). */
+void mha_hd64_set_stamp_buffer(void* p);
+/* How the calling thread's last launch merged its KV splits: 0 no split, 1 in-launch, 2 kernel. */
+int32_t mha_hd64_last_combine_form(void);
 
 #ifdef __cplusplus
 }  /* extern "C" */

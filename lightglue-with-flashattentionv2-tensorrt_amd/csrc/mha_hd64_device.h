@@ -279,16 +279,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, un
 // the compiler cannot tell the DMA's LDS writes from later ds_read_b64_tr_b16 reads of any address
 // and drains EVERY DMA in flight, vmcnt(0), before the first transposing read.)
 // m0 / soff are wave-uniform; readfirstlane pins values the compiler computed on the vector unit
-// into the SGPRs the "s" constraints need.
+// into the SGPRs the "s" constraints need. M0 is an explicit "{m0}" operand: the compiler writes
+// it itself and knows the statement reads it (no value of its own is kept there across the asm).
+// `s_nop 4` gives the 5 wait states a VMEM read of an SGPR (soffset, descriptor, M0) needs after a
+// VALU (v_readfirstlane) or SALU wrote it — the compiler's hazard recognizer does not look inside
+// the asm (as masked_load_dword below).
 __device__ __forceinline__ void lds_dma16(unsigned m0, unsigned voff, __amdgpu_buffer_rsrc_t rs, unsigned soff) {
     m0 = __builtin_amdgcn_readfirstlane(m0);
     soff = __builtin_amdgcn_readfirstlane(soff);
     asm volatile(
-        "s_mov_b32 m0, %0\n\t"
-        "s_nop 0\n\t"
-        "buffer_load_dwordx4 %1, %2, %3 offen lds"
+        "s_nop 4\n\t"
+        "buffer_load_dwordx4 %0, %1, %2 offen lds"
         :
-        : "s"(m0), "v"(voff), "s"(rs), "s"(soff)
+        : "v"(voff), "s"(rs), "s"(soff), "{m0}"(m0)
         : "memory");
 }
 // LDS byte address of a pointer into a __shared__ array (the value M0 takes)

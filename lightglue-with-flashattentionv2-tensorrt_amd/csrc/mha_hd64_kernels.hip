@@ -986,14 +986,15 @@ static unsigned* tickets_for(hipStream_t stream, int count) {
     // 512 Ki tickets recorded with no eager launch in between.
     RelaxedCapture relaxed;
     if (!ar.base || (ar.used > ar.cap / 2 && ar.replaced < kMaxArenas)) {
-        if (ar.base) ++ar.replaced;
         unsigned* fresh = zeroed_tickets(kArenaTickets, stream);
         if (fresh && hipStreamSynchronize(stream) == hipSuccess) {
+            if (ar.base) ++ar.replaced;  // (counted only once a fresh arena is installed)
             ar.base = fresh;
             ar.cap = kArenaTickets;
             ar.used = 0;
-        } else if (!ar.base) {
-            ar.cap = 0;
+        } else {
+            if (fresh) (void)hipFree(fresh);  // a failed attempt leaks nothing
+            if (!ar.base) ar.cap = 0;
         }
     }
     auto& slot = g_tickets[{dev, stream}];

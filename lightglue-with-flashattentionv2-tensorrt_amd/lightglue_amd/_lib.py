@@ -137,17 +137,17 @@ SIGNATURES.update({
     "lg_layernorm_gelu": ([_I, _P, _P, _P, _I, _I, ctypes.c_float, _P, _P], _I),
     "lg_log_double_softmax_workspace": ([_I, _I], _S),
     "lg_log_double_softmax": ([_P, _P, _P, _I, _I, _P, _P, _P], _I),
-})
-# Test/bench hooks exported by the library but not part of the public header.
-HOOKS = {
-    "mha_hd64_launch_forced": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _S, _P, _I], _I),
-    "mha_hd64_plan": ([_I, _I, _I, _I, _S, ctypes.POINTER(ctypes.c_int32)], _S),
-    "mha_hd64_set_stamp_buffer": ([_P], None),
+    # kernel-form switches (include/mha_hd64.h "kernel-form switches")
     "mha_hd64_set_fused_combine": ([_I], None),
     "mha_hd64_set_f32_inkernel": ([_I], None),
     "mha_hd64_set_stream_mode": ([_I], None),
+    # test and benchmark hooks (include/mha_hd64.h "test and benchmark hooks")
+    "mha_hd64_launch_forced": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _S, _P, _I], _I),
+    "mha_hd64_plan": ([_I, _I, _I, _I, _S, ctypes.POINTER(ctypes.c_int32)], _S),
+    "mha_hd64_set_stamp_buffer": ([_P], None),
     "mha_hd64_last_combine_form": ([], _I),
-}
+})
+HOOKS = {}  # (every export is declared in include/mha_hd64.h since round 4)
 
 _lib = None
 

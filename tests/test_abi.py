@@ -61,6 +61,9 @@ def test_every_header_symbol_is_exported(lib):
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T ((?:mha_hd64|lg)_\w+)", out))
     assert set(names) <= exported
+    # ... and the other way round: no exported C entry point lacks a prototype a C host can bind
+    undeclared = sorted(exported - set(names))
+    assert not undeclared, f"exported without a declaration in include/*.h: {undeclared}"
 
 
 def test_library_is_gfx950_code_object(lib):

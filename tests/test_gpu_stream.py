@@ -125,7 +125,7 @@ def test_stream_kernel_large_negative_logits(dev, oracle_mod):
     """Scores far below zero everywhere (~ -200 raw, as test_gpu_parity.py's case) in a launch of
     several items per workgroup: each item's first tile must set its max (no underflow to l = 0).
     At this logit scale the fp16 operands of Q·Kᵀ alone put every plan ~6e-3 from the fp64 oracle
-    (tools/_extreme_logits.py: identical errors across plans 0/1/21/22/23), so both output types
+    (tools/extreme_logits.py: identical errors across plans 0/1/21/22/23), so both output types
     take the 1e-2 contract here, and the stream kernel must agree with the planner's plan."""
     from lightglue_amd import _lib, synth
 

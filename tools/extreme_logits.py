@@ -1,4 +1,4 @@
-"""Scratch diagnostic: max-abs error vs the C oracle of each plan on extreme logits (|q| x 40)."""
+"""Diagnostic: max-abs error vs the C oracle of each plan on extreme logits (|q| x 40)."""
 import os, sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "lightglue-with-flashattentionv2-tensorrt_amd")]
