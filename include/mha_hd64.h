@@ -222,10 +222,10 @@ int32_t mha_hd64_set_concurrency_hint(int32_t streams);
 /* ---- kernel-form switches (no reference counterpart; process-wide, thread-safe, take effect at
  * the next launch; every setting gives results within the same tolerance of the oracle) ---- */
 /* Throughput kernel for launches that carry more than one round of 128-row query blocks (batched
- * image-pair streams, grouped layers of several pairs): 1 = the persistent streaming kernel
- * (fp16 inputs; the planner default where it measured faster),
- * 0 = the LDS-ring kernel. The environment variable MHA_HD64_STREAM=0/1 sets the initial value. */
-void mha_hd64_set_stream_mode(int32_t mode);
+ * image-pair streams, grouped layers of several pairs): 1 (default) = the persistent streaming
+ * kernel (fp16 inputs), 0 = the LDS-ring kernel. The environment variable
+ * MHA_HD64_STREAM=0/1 sets the initial value. Returns the previous mode. */
+int32_t mha_hd64_set_stream_mode(int32_t mode);
 /* FLOAT (fp32) inputs: 1 (default) = rounded to fp16 inside the attention kernel where that
  * measured faster (one launch), 0 = always a convert launch into the workspace + the fp16 kernel,
  * 2 = also the two-pass in-kernel forms (1024 < nkv <= 2048; diagnostic, measured slower).

@@ -91,7 +91,7 @@ int32_t report_error(int32_t status, const char* where, const char* what);
 void set_stamp_buffer(void* p);
 // In-launch split combine on/off (default on unless env MHA_HD64_FUSED_COMBINE=0).
 void set_fused_combine(int enable);
-void set_stream_mode(int mode);     // 1 = persistent streaming kernel for large fp16 launches
+int set_stream_mode(int mode);      // 1 = persistent streaming kernel for large fp16 launches; returns the previous
 void set_f32_inkernel(int enable);  // fp32 inputs: 1 = rounded in the 16-row kernel, 0 = convert launch,
                                     // 2 = also the two-pass forms (diagnostic)
 // How the calling thread's last launch merged its splits: 0 none, 1 in-launch, 2 combine kernel.

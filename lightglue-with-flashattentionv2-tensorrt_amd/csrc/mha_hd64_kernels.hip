@@ -1063,27 +1063,19 @@ static bool direct16_enabled() {
     return on;
 }
 
-// The persistent streaming kernel (mha_hd64_stream.hip) for launches of many 128-row blocks
-// (MHA_HD64_STREAM=0 / set_stream_mode(0): never (default); 1: for every fp16 launch past one round
-// of 128-row blocks). Opt-in: it ties the ring kernel from 16 batched calls up and loses below
-// (DESIGN.md section 8.5).
+// The persistent streaming kernel (mha_hd64_stream.hip) for fp16 launches of more than one round
+// of 128-row blocks (MHA_HD64_STREAM=1 / set_stream_mode(1), the default; 0: never). Round 4's
+// branch-free step loop: 16 batched 1x4x1024^2 calls 23.6 vs 26.0 us for the ring kernel, 32
+// calls 44.2 vs 49.8 (profiles/r04/stream_check.jsonl).
 std::atomic<int> g_stream_mode{-1};
 int stream_env() {
     int v = g_stream_mode.load();
     if (v < 0) {
         const char* e = std::getenv("MHA_HD64_STREAM");
         int expect = -1;
-        g_stream_mode.compare_exchange_strong(expect, (e && e[0] == '1') ? 1 : 0);
+        g_stream_mode.compare_exchange_strong(expect, (e && e[0] == '0') ? 0 : 1);
         v = g_stream_mode.load();
     }
-    return v;
-}
-// waves per streaming workgroup (MHA_HD64_STREAM_WAVES=8: 256-row items; default 4, the faster)
-static int stream_waves() {
-    static const int v = [] {
-        const char* e = std::getenv("MHA_HD64_STREAM_WAVES");
-        return (e && e[0] == '8') ? 8 : 4;
-    }();
     return v;
 }
 static bool stream_auto(const Call* calls, int n, InType in) {
@@ -1098,7 +1090,7 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
     GroupPlan p{};
     if (force_q_waves == kForceStream || (force_q_waves == 0 && stream_auto(calls, n, in))) {
         if (in == InType::F16) {
-            p.q_waves = stream_waves();  // 128- or 256-row items
+            p.q_waves = 4;  // 128-row items
             p.kv_waves = 1;
             p.rows_per_wave = 32;
             p.stream = 1;
@@ -1303,7 +1295,11 @@ bool f32_inkernel_two_pass() { return f32_inkernel_enabled() && g_f32_inkernel.l
 }  // namespace
 
 void set_f32_inkernel(int enable) { g_f32_inkernel.store(enable <= 0 ? 0 : enable >= 2 ? 2 : 1); }
-void set_stream_mode(int mode) { g_stream_mode.store(mode ? 1 : 0); }
+int set_stream_mode(int mode) {
+    const int prev = stream_env();
+    g_stream_mode.store(mode ? 1 : 0);
+    return prev;
+}
 
 static hipError_t launch_group_chunk(const Call* calls, int n, InType in, OutType out, void* workspace,
                                      size_t ws_bytes, hipStream_t stream, int force_q_waves, int force_kv_waves,

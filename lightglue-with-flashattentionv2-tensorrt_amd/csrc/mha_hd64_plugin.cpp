@@ -423,9 +423,9 @@ void mha_hd64_set_fused_combine(int32_t enable) { mha_hd64::set_fused_combine(en
 // Test/bench hook: fp32 Q/K/V rounded to fp16 inside the 16-row kernel (1, default where it
 // applies) or by a separate convert launch before the fp16 kernel (0); results are bitwise equal.
 void mha_hd64_set_f32_inkernel(int32_t enable) { mha_hd64::set_f32_inkernel(enable); }
-// Test/bench hook: 1 = the persistent streaming kernel for fp16 launches of > 256 128-row blocks,
-// 0 = never (default; MHA_HD64_STREAM=1 sets 1 at first use).
-void mha_hd64_set_stream_mode(int32_t mode) { mha_hd64::set_stream_mode(mode); }
+// 1 = the persistent streaming kernel for fp16 launches of > 256 128-row blocks (default),
+// 0 = never (MHA_HD64_STREAM=0 sets 0 at first use). Returns the previous mode.
+int32_t mha_hd64_set_stream_mode(int32_t mode) { return mha_hd64::set_stream_mode(mode); }
 // Test hook: 0 = the calling thread's last launch had no split, 1 = in-launch combine, 2 = combine kernel.
 int32_t mha_hd64_last_combine_form(void) { return mha_hd64::last_combine_form(); }
 

@@ -140,7 +140,7 @@ SIGNATURES.update({
     # kernel-form switches (include/mha_hd64.h "kernel-form switches")
     "mha_hd64_set_fused_combine": ([_I], None),
     "mha_hd64_set_f32_inkernel": ([_I], None),
-    "mha_hd64_set_stream_mode": ([_I], None),
+    "mha_hd64_set_stream_mode": ([_I], _I),
     # test and benchmark hooks (include/mha_hd64.h "test and benchmark hooks")
     "mha_hd64_launch_forced": ([_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _S, _P, _I], _I),
     "mha_hd64_plan": ([_I, _I, _I, _I, _S, ctypes.POINTER(ctypes.c_int32)], _S),

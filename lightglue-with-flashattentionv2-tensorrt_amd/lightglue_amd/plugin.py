@@ -233,13 +233,12 @@ def set_concurrency_hint(streams: int) -> int:
     return int(_lib.load().mha_hd64_set_concurrency_hint(int(streams)))
 
 
-def set_stream_mode(mode: int) -> None:
-    """1: fp16 launches of more than 256 128-row blocks (batched image-pair streams, large grouped
-    layers) run the persistent streaming kernel (csrc/mha_hd64_stream.hip); 0 (default): the
-    planner's other plans. Same results within the contract; measured a tie with the LDS-ring
-    kernel at 16-32 calls per launch. Process-wide (MHA_HD64_STREAM=1 sets
-    1 at first use)."""
-    _lib.load().mha_hd64_set_stream_mode(int(mode))
+def set_stream_mode(mode: int) -> int:
+    """1 (default): fp16 launches of more than 256 128-row blocks (batched image-pair streams,
+    large grouped layers) run the persistent streaming kernel (csrc/mha_hd64_stream.hip); 0: the
+    planner's other plans (the LDS-ring kernel there). Same results within the contract (DESIGN.md
+    section 3). Process-wide (MHA_HD64_STREAM=0 sets 0 at first use). Returns the previous mode."""
+    return int(_lib.load().mha_hd64_set_stream_mode(int(mode)))
 
 
 def _require_gpu(*ts: torch.Tensor) -> None:

@@ -1047,8 +1047,7 @@ def test_grouped_random_groups(mode, dev, oracle_mod):
     lib = _lib.load()
     rng = np.random.default_rng({"default": 31, "hint3": 32, "stream": 33}[mode])
     prev_hint = lightglue_amd.set_concurrency_hint(3) if mode == "hint3" else None
-    if mode == "stream":
-        lib.mha_hd64_set_stream_mode(1)
+    prev_stream = lib.mha_hd64_set_stream_mode(1 if mode == "stream" else 0)
     try:
         for case in range(10):
             n_calls = int(rng.integers(1, 7))
@@ -1081,8 +1080,7 @@ def test_grouped_random_groups(mode, dev, oracle_mod):
     finally:
         if prev_hint is not None:
             lightglue_amd.set_concurrency_hint(prev_hint)
-        if mode == "stream":
-            lib.mha_hd64_set_stream_mode(0)
+        lib.mha_hd64_set_stream_mode(prev_stream)
 
 
 @pytest.mark.parametrize("heads", [1, 2, 3, 8])
@@ -1095,7 +1093,7 @@ def test_batched_launcher_other_head_counts(heads, dev, oracle_mod):
 
     shapes = [(1, 1024, 1024), (2, 1000, 777), (1, 100, 2048), (12, 1024, 1024), (1, 33, 65)]
     for mode in (0, 1):
-        lightglue_amd.set_stream_mode(mode)
+        prev_stream = lightglue_amd.set_stream_mode(mode)
         try:
             for i, (b, nq, nkv) in enumerate(shapes):
                 qn, kn, vn = synth.qkv(7100 + 31 * i + heads, nq, nkv, batch=b, heads=heads)
@@ -1113,4 +1111,4 @@ def test_batched_launcher_other_head_counts(heads, dev, oracle_mod):
                     d = _maxdiff(got[bsel][:, :, rows], ref)
                     assert d <= tol, (heads, b, nq, nkv, mode, out_dt, d)
         finally:
-            lightglue_amd.set_stream_mode(0)
+            lightglue_amd.set_stream_mode(prev_stream)

@@ -34,8 +34,10 @@ def dev():
 def stream_mode(dev):
     import lightglue_amd
 
+    prev = lightglue_amd.set_stream_mode(1)
+    lightglue_amd.set_stream_mode(prev)
     yield lightglue_amd.set_stream_mode
-    lightglue_amd.set_stream_mode(0)
+    lightglue_amd.set_stream_mode(prev)
 
 
 def _t(x, dev, dtype):

@@ -34,25 +34,43 @@ for _ in range(20):
     assert lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), B, 4, nq, nkv, 0, 0, 23,
                                       0, 0, ws.data_ptr(), ws.numel(), s, 3) == 0
 torch.cuda.synchronize()
-W = int(os.environ.get("MHA_HD64_STREAM_WAVES", "8"))
+W = int(os.environ.get("MHA_HD64_STREAM_WAVES", "4"))
 items = B * 4 * -(-nq // (32 * W))
 grid = min(items, 512 if W == 4 else 256)
 t = st[: grid * W * 16].view(grid * W, 16).cpu().numpy().astype(np.float64)
-steps = t[:, 6]
-per = t[:, :6] / np.maximum(steps, 1)[:, None]
-names = ["refill_issue", "decision", "phaseA", "phaseB", "dma_wait", "barrier"]
-out = {"batch": B, "nq": nq, "nkv": nkv, "grid": grid, "steps_per_wave_med": float(np.median(steps))}
-for i, n in enumerate(names):
-    out[n] = {"med": round(float(np.median(per[:, i])), 1), "p90": round(float(np.percentile(per[:, i], 90)), 1)}
-out["step_total_med"] = round(float(np.median(per.sum(1))), 1)
+# layout (csrc/mha_hd64_stream.hip, MHA_STREAM_STAMPS): 0 the first item's tile 0 (kernel
+# prologue), 1 first steps, 2 middle loop, 3 tail + last steps + epilogues, 6 middle steps, 14
+# items, 8..11 entry / exit clocks, 12 end of the kernel prologue's loads
+items = np.maximum(t[:, 14], 1)
+nmid = np.maximum(t[:, 6], 1)
+out = {"batch": B, "nq": nq, "nkv": nkv, "grid": grid, "waves": W, "items_per_wave_med": float(np.median(t[:, 14])),
+       "middle_steps_per_wave_med": float(np.median(t[:, 6]))}
+out["first_tile0_cyc_med"] = round(float(np.median(t[:, 0])), 1)
+out["first_step_cyc_med"] = round(float(np.median(t[:, 1] / items)), 1)
+out["middle_step_cyc_med"] = round(float(np.median(t[:, 2] / nmid)), 1)
+out["tail_last_epilogue_cyc_med"] = round(float(np.median(t[:, 3] / items)), 1)
 life = t[:, 10] - t[:, 8]
 real = (t[:, 11] - t[:, 9]) / 100.0  # us at 100 MHz
 out["wave_life_cyc_med"] = float(np.median(life))
-out["in_steps_frac_med"] = round(float(np.median(t[:, :6].sum(1) / np.maximum(life, 1))), 3)
+pro = t[:, 12] - t[:, 8]
+out["kernel_prologue_cyc_med"] = float(np.median(pro))
+acc = pro + t[:, 0] + t[:, 1] + t[:, 2] + t[:, 3]
+out["accounted_frac_med"] = round(float(np.median(acc / np.maximum(life, 1))), 3)
+out["middle_frac_med"] = round(float(np.median(t[:, 2] / np.maximum(life, 1))), 3)
 out["clock_ghz_med"] = round(float(np.median(life / np.maximum(real, 1e-9) / 1e3)), 3)
-out["prologue_cyc_med"] = float(np.median(t[:, 12] - t[:, 8]))
-out["epilogues_cyc_med"] = float(np.median(t[:, 13]))
-out["entry_spread_cyc"] = float(t[:, 8].max() - t[:, 8].min())
-out["exit_spread_cyc"] = float(t[:, 10].max() - t[:, 10].min())
 out["kernel_span_us"] = round(float((t[:, 11].max() - t[:, 9].min()) / 100.0), 2)
+# launch timeline on the global 100 MHz clock: when waves start and end relative to the first start
+t0 = t[:, 9].min()
+ent = (t[:, 9] - t0) / 100.0
+ext = (t[:, 11] - t0) / 100.0
+out["entry_us_p50_p90_max"] = [round(float(np.percentile(ent, q)), 2) for q in (50, 90, 100)]
+out["exit_us_min_p10_p50_max"] = [round(float(np.percentile(ext, q)), 2) for q in (0, 10, 50, 100)]
+out["wave_life_us_min_p50_max"] = [round(float(np.percentile(real, q)), 2) for q in (0, 50, 100)]
+# by XCD (blockIdx % 8 under round-robin placement) and by half of the grid
+wg = np.arange(grid * W) // W
+clk = life / np.maximum(real, 1e-9) / 1e3
+out["life_us_by_xcd"] = [round(float(np.median(real[wg % 8 == x])), 2) for x in range(8)]
+out["clock_ghz_by_xcd"] = [round(float(np.median(clk[wg % 8 == x])), 3) for x in range(8)]
+out["life_us_by_half"] = [round(float(np.median(real[wg < grid // 2])), 2), round(float(np.median(real[wg >= grid // 2])), 2)]
+out["middle_cyc_by_xcd"] = [round(float(np.median((t[:, 2] / nmid)[wg % 8 == x])), 1) for x in range(8)]
 print(json.dumps(out))
