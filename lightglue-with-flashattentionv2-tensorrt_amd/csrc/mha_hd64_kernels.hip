@@ -1090,8 +1090,20 @@ GroupPlan plan_group(const Call* calls, int n, size_t ws_bytes, int force_q_wave
     GroupPlan p{};
     if (force_q_waves == kForceStream || (force_q_waves == 0 && stream_auto(calls, n, in))) {
         if (in == InType::F16) {
-            p.q_waves = 4;  // 128-row items
-            p.kv_waves = 1;
+            // 8 waves (256-row items, one workgroup per CU: the two waves of a SIMD stay in step, no
+            // co-resident imbalance) when their last round of 256 items is at least 3/4 full; else
+            // 4 (128-row items, two per CU: the older workgroup of a CU takes the extra items of a
+            // partial round). tools/stream_check.py, 1024^2 calls per launch, us: 12 calls 20.0 vs
+            // 21.1, 16: 22.5 vs 23.4, 24: 38.5 vs 34.0, 32: 43.3 vs 44.7, 64: 81.1 vs 84.3.
+            // force_kv_waves 4 / 8 (forced plan 23) picks one.
+            long blocks256 = 0;
+            for (int i = 0; i < n; ++i) blocks256 += (long)calls[i].batch * calls[i].heads * ((calls[i].nq + 255) / 256);
+            const long rounds8 = (blocks256 + 255) / 256;
+            const int nw = (force_q_waves == kForceStream && (force_kv_waves == 4 || force_kv_waves == 8))
+                               ? force_kv_waves
+                               : (4 * (256 * rounds8 - blocks256) <= 256 ? 8 : 4);
+            p.q_waves = nw;  // items of 32·nw rows
+            p.kv_waves = nw;  // (reported by the plan query)
             p.rows_per_wave = 32;
             p.stream = 1;
             for (int i = 0; i < n; ++i) {

@@ -56,28 +56,47 @@
 #include "mha_hd64_internal.h"
 
 // Diagnostic build (-DMHA_STREAM_STAMPS, tools/stream_stamps.py): per wave, s_memtime cycles by
-// part, written at exit to a.stamps[(blockIdx.x * 4 + wave) * 16 + k]: 0 item prologues, 1 first
+// part, written at exit to a.stamps[(blockIdx.x * 4 + wave) * 48 + k]: 0 item prologues, 1 first
 // steps, 2 middle-loop steps, 3 tail + last steps + epilogues, 6 middle steps counted, 14 items,
 // 8..11 s_memtime / s_memrealtime (100 MHz) at entry and exit (the in-kernel clock,
-// MI355X_MICROARCH.md DVFS item 6), 12 the end of the kernel prologue.
+// MI355X_MICROARCH.md DVFS item 6), 12 the end of the kernel prologue; 16 + k chained segments
+// (SEG(k): 0 item advance, 1 next Q issue, 2..5 FIRST step phase A / phase B / mask+max+epilogue
+// +wait / barrier, 6..9 the same for middle steps, 10..13 tail steps, 14 to the last step, 15 read_q,
+// 16..19 the LAST step).
 #ifdef MHA_STREAM_STAMPS
 #define SCLK(var) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
+// chained segments: sg[k] += cycles since the previous SEG stamp (written to slots 16 + k)
+#define SEG(k)                                      \
+    do {                                            \
+        unsigned long long t_;                      \
+        SCLK(t_);                                   \
+        sg[k] += (unsigned)(t_ - ck_last);          \
+        ck_last = t_;                               \
+    } while (0)
 #else
 #define SCLK(var) \
     do {          \
     } while (0)
+#define SEG(k) \
+    do {       \
+    } while (0)
 #endif
+constexpr int kStreamStampSlots = 48;  // per wave, diagnostic builds
 
 namespace mha_hd64 {
 namespace {
 
-constexpr int kSW = 4;                         // waves per workgroup
-constexpr int kSRows = 32 * kSW;               // query rows per item
+// NW waves per workgroup (4: 128-row items, two workgroups per CU; 8: 256-row items sharing each
+// K/V tile, one workgroup per CU)
+template <int NW>
+constexpr int stream_rows() { return 32 * NW; }  // query rows per item
 constexpr int kSSlot = 2 * kTileBytes;         // one ring slot: K image, then V image (16 KiB)
 constexpr int kSSlots = 4;                     // ring slots
-constexpr int kSQOff = kSSlots * kSSlot;       // Q region: the item's 128 rows (16 KiB)
-constexpr int kSLds = kSQOff + kSRows * 128;   // 80 KiB: two workgroups per CU
-constexpr int kSMaxGrid = 512;
+constexpr int kSQOff = kSSlots * kSSlot;       // Q region: the item's rows (16 / 32 KiB)
+template <int NW>
+constexpr int stream_lds() { return kSQOff + stream_rows<NW>() * 128; }  // 80 KiB (NW 4) / 96 KiB (NW 8)
+template <int NW>
+constexpr int stream_max_grid() { return NW == 4 ? 512 : 256; }  // one residency round
 
 // Call ci's arguments, field by field with compile-time indices (a runtime index into the
 // kernarg table would copy it to scratch).
@@ -116,15 +135,25 @@ struct StreamItem {
     int nt;  // 64-key tiles, rounded up to an even count (the padding tile reads zeros, masked)
 };
 
-template <bool MULTI, int OSZ>
+template <bool MULTI, int OSZ, int NW>
 __device__ __forceinline__ StreamItem stream_item(const FwdArgs& a, int j, bool live) {
     const int ci = stream_call<MULTI>(a, j);
     const int nq = MHA_SEL(nq), nkv = MHA_SEL(nkv), qtiles = MHA_SEL(qtiles);
     const int jl = j - MHA_SEL(block_begin);
     const int bh = jl / qtiles, qtile = jl - bh * qtiles;
-    const char* q = reinterpret_cast<const char*>(MHA_SEL(q)) + (size_t)bh * nq * (kHeadDim * 2);
-    const char* k = reinterpret_cast<const char*>(MHA_SEL(k)) + (size_t)bh * nkv * (kHeadDim * 2);
-    const char* v = reinterpret_cast<const char*>(MHA_SEL(v)) + (size_t)bh * nkv * (kHeadDim * 2);
+#ifdef MHA_STREAM_L2KV  // diagnostic: every item streams the first head's K/V (L2-resident)
+    const int bhk = 0;
+#else
+    const int bhk = bh;
+#endif
+#ifdef MHA_STREAM_L2Q  // diagnostic: every item reads the first query block (L2-resident)
+    const int bhq = 0;
+#else
+    const int bhq = bh;
+#endif
+    const char* q = reinterpret_cast<const char*>(MHA_SEL(q)) + (size_t)bhq * nq * (kHeadDim * 2);
+    const char* k = reinterpret_cast<const char*>(MHA_SEL(k)) + (size_t)bhk * nkv * (kHeadDim * 2);
+    const char* v = reinterpret_cast<const char*>(MHA_SEL(v)) + (size_t)bhk * nkv * (kHeadDim * 2);
     char* o = reinterpret_cast<char*>(MHA_SEL(o)) + (size_t)bh * nq * (kHeadDim * OSZ);
     StreamItem it;
     // (a dead item — past the workgroup's last — gets empty descriptors: its DMA pieces read zeros)
@@ -134,7 +163,11 @@ __device__ __forceinline__ StreamItem stream_item(const FwdArgs& a, int j, bool 
     it.q = stream_rsrc(q, live ? (unsigned)nq * kHeadDim * 2 : 0u);
     it.o = stream_rsrc(o, (unsigned)nq * kHeadDim * OSZ);
     it.nkv = nkv;
-    it.q0 = qtile * kSRows;
+#ifdef MHA_STREAM_L2Q
+    it.q0 = 0;
+#else
+    it.q0 = qtile * stream_rows<NW>();
+#endif
     it.nt = ((nkv + 2 * kTileKV - 1) / (2 * kTileKV)) * 2;
     return it;
 }
@@ -163,10 +196,11 @@ struct StreamScores {
     bool rs;        // some query of the wave exceeds the running max by > kRescaleThr (wave-uniform)
 };
 
-template <typename TOut, bool MULTI>
-__global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a) {
+template <typename TOut, bool MULTI, int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kernel(FwdArgs a) {
     constexpr int OSZ = (int)sizeof(TOut);
-    __shared__ __attribute__((aligned(1024))) char smem[kSLds];
+    constexpr int kPW = 8 / NW;  // DMA pieces (1 KiB, 8 rows) per wave of each 8 KiB K or V image
+    __shared__ __attribute__((aligned(1024))) char smem[stream_lds<NW>()];
     lds_char* const lds = (lds_char*)smem;
     const unsigned lds0 = (unsigned)(uintptr_t)lds;
 
@@ -178,7 +212,10 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
 
 #ifdef MHA_STREAM_STAMPS
     unsigned long long ck_entry[2], ck_pro = 0, ck_t0 = 0, ck_t1 = 0;
-    unsigned long long ck_sum[4] = {0, 0, 0, 0}, ck_mid = 0, ck_items = 0;
+    unsigned long long ck_sum[4] = {0, 0, 0, 0}, ck_mid = 0, ck_items = 0, ck_last = 0;
+    unsigned sg[24];
+#pragma unroll
+    for (int i_ = 0; i_ < 24; ++i_) sg[i_] = 0;
     asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(ck_entry[0]), "=s"(ck_entry[1])::"memory");
 #endif
     // This workgroup's items: XCD x = blockIdx % 8 owns the contiguous range [jb, je) of the T
@@ -191,13 +228,6 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
     const int G = ((int)gridDim.x - xcd + 7) >> 3;
     int j = jb + loc;
     if (j >= je) return;  // (grid <= items: never)
-#ifndef MHA_STREAM_PRIO
-#define MHA_STREAM_PRIO 0
-#endif
-    // the second-dispatched half of the grid: the other workgroup on each CU (the arbitration
-    // loser on age, MI355X_MICROARCH.md "Two waves per SIMD" item 2)
-    const unsigned half = (unsigned)__builtin_amdgcn_readfirstlane(blockIdx.x >= gridDim.x / 2 ? 1 : 0);
-    (void)half;
 
     // ---- per-lane constant addressing ----
     // K image (A operand of Sᵀ = K·Qᵀ): dim step s, half-wave hh reads chunk 2s + hh of key row r
@@ -232,10 +262,12 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
     auto issue_tile = [&](const StreamItem& it, int lt, unsigned slot) {
         const unsigned m = m0w + slot * (unsigned)kSSlot;
         const unsigned so = (unsigned)lt * (unsigned)kTileBytes + sow;
-        lds_dma16(m, dma_k, it.k, so);
-        lds_dma16(m + 4096u, dma_k, it.k, so + 4096u);
-        lds_dma16(m + (unsigned)kTileBytes, dma_v, it.v, so);
-        lds_dma16(m + (unsigned)kTileBytes + 4096u, dma_v, it.v, so + 4096u);
+#pragma unroll
+        for (int h = 0; h < kPW; ++h) {  // pieces wave + NW·h of each image (8 KiB apart per image)
+            const unsigned ho = (unsigned)(h * NW * 1024);
+            lds_dma16(m + ho, dma_k, it.k, so + ho);
+            lds_dma16(m + (unsigned)kTileBytes + ho, dma_v, it.v, so + ho);
+        }
     };
     // this wave's 32 Q rows of an item into its part of the Q region
     const unsigned q_m0 = (unsigned)__builtin_amdgcn_readfirstlane(lds0 + q_base);
@@ -246,8 +278,8 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
     };
 
     // ---- state ----
-    StreamItem cur = stream_item<MULTI, OSZ>(a, j, true);
-    StreamItem nxt = stream_item<MULTI, OSZ>(a, j + G < je ? j + G : j, j + G < je);
+    StreamItem cur = stream_item<MULTI, OSZ, NW>(a, j, true);
+    StreamItem nxt = stream_item<MULTI, OSZ, NW>(a, j + G < je ? j + G : j, j + G < je);
     unsigned gb = 0;  // global tile index of the current item's tile 0 (ring slot = index mod 4)
     f16x8 qf[4];
     f32x16 cm;                  // −m (the QKᵀ chains' C operand)
@@ -262,7 +294,7 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
     issue_tile(cur, 0, 0u);
     issue_tile(cur, 1, 1u);
 #pragma unroll
-    for (unsigned off = (unsigned)tid * 16u; off < (unsigned)kTileBytes; off += 64u * kSW * 16u)
+    for (unsigned off = (unsigned)tid * 16u; off < (unsigned)kTileBytes; off += 64u * NW * 16u)
         lds_write16(lds, 3u * (unsigned)kSSlot + (unsigned)kTileBytes + off, f16x8{});
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj)
@@ -272,6 +304,7 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
     __builtin_amdgcn_s_barrier();
 #ifdef MHA_STREAM_STAMPS
     SCLK(ck_pro);
+    ck_last = ck_pro;
 #endif
 
     auto mask_tile = [&](StreamScores& s, int lim) {  // keys >= lim of the tile -> -inf
@@ -368,18 +401,6 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
         constexpr bool LAST = KIND == 3;
         constexpr bool MASK = KIND == 0 || KIND >= 2;  // tile t + 1 may hold keys past nkv
         const unsigned g = gb + (unsigned)t;
-#if MHA_STREAM_PRIO == 1
-        // A/B: the two workgroups of a CU alternate the issue priority step by step
-        if (((unsigned)t ^ half) & 1u) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-#elif MHA_STREAM_PRIO == 2
-        {  // A/B: ... in windows of 4096 cycles of the shared clock
-            unsigned long long tnow;
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tnow)::"memory");
-            if ((((unsigned)(tnow >> 12)) ^ half) & 1u) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-#endif
         const unsigned kbase = ((g + 1u) & 3u) * (unsigned)kSSlot;  // K of tile t + 1
         const unsigned vbase = ((g - 1u) & 3u) * (unsigned)kSSlot;  // V of tile t − 1
         // FIRST: tile 0's scores came from a C = 0 chain (the previous item's last step, or the
@@ -409,10 +430,10 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
         const __amdgpu_buffer_rsrc_t rv_ = own ? cur.v : nxt.v;
         const unsigned fm = m0w + ((g + 2u) & 3u) * (unsigned)kSSlot;
         const unsigned fso = (unsigned)lt * (unsigned)kTileBytes + sow;
-        auto dma = [&](int i) {  // piece i of the refill: K w, K w+4, V w, V w+4
-            const unsigned hi = (i & 1) ? 4096u : 0u;
-            if (i < 2) lds_dma16(fm + hi, dma_k, rk_, fso + hi);
-            else lds_dma16(fm + (unsigned)kTileBytes + hi, dma_v, rv_, fso + hi);
+        auto dma = [&](int i) {  // piece i (< 2 kPW) of the refill: K w, (K w+4,) V w(, V w+4)
+            const unsigned ho = (unsigned)((i % kPW) * NW * 1024);
+            if (i < kPW) lds_dma16(fm + ho, dma_k, rk_, fso + ho);
+            else lds_dma16(fm + (unsigned)kTileBytes + ho, dma_v, rv_, fso + ho);
         };
 
         // ---- vector work, a fixed order over the step's MFMA gaps ----
@@ -454,6 +475,7 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
             if (gi >= 14 && gi < 18) maxk(gi - 14);
         };
 
+        constexpr int SB = KIND == 0 ? 2 : KIND == 1 ? 6 : KIND == 2 ? 10 : 16;  // (stamps: segment base)
         int gi = 0;
         // phase A: QKᵀ(t + 1), each gap an exponential pair (+ LDS reads, DMA pieces, packs). In
         // the LAST step, tile t + 1 is the next item's tile 0 (global tile g + 1, landed two
@@ -479,11 +501,12 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
                         if (s == 1) read_v(vbase, 0);
                         if (s == 2) read_v(vbase, 1);
                     }
-                    dma(s);
+                    if (s < 2 * kPW) dma(s);
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
+        SEG(SB);
         // phase B: Oᵀ += Vᵀ·Pᵀ(t − 1) and its row sums (each gap a pack, the rest of the
         // exponentials, the row max of tile t + 1)
 #pragma unroll
@@ -502,6 +525,7 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
         // P of tile t is consumed only by the next step: without this tie the compiler sinks the
         // exponentials and packs past the barrier, where no MFMA runs beside them
         asm volatile("" : "+v"(pn[0][0]), "+v"(pn[0][1]), "+v"(pn[1][0]), "+v"(pn[1][1]));
+        SEG(SB + 1);
         if constexpr (MASK) {  // LAST: the next item's tile 0 (keys past its nkv)
             const int lim = LAST ? nxt.nkv : cur.nkv - kTileKV * (t + 1);  // keys of tile t + 1 (<= 0: none)
             if (lim < kTileKV) {  // (wave-uniform, rare: a partial or padding tile)
@@ -533,8 +557,10 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the refill has landed
         }
+        SEG(SB + 2);
         // ... then every wave's
         __builtin_amdgcn_s_barrier();
+        SEG(SB + 3);
     };
 
     using K0 = std::integral_constant<int, 0>;
@@ -574,8 +600,10 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
 #endif
     for (;;) {
         // the next item's Q rows of this wave, once its reads of the region have returned
+        SEG(0);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         issue_q(nxt);
+        SEG(1);
         const int nt = cur.nt;
         const int nfull = cur.nkv / kTileKV;  // tiles without keys past nkv
         // step 0 (nt >= 2): with the previous item's last P·V and epilogue
@@ -605,7 +633,9 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
         // the last step: beside tile nt − 2's P·V, the next item's tile 0 (its Q first: the
         // current item's fragments are no longer needed); tile nt − 1's P·V and this item's
         // epilogue follow in the next item's FIRST step
+        SEG(14);
         const unsigned qbad_next = read_q();
+        SEG(15);
         step(K3{}, t, sB, sA, pA, pB);
 #ifdef MHA_STREAM_STAMPS
         SCLK(ck_t1);
@@ -624,7 +654,7 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
         cur = nxt;
         qbad = qbad_next;
         const bool more = j + G < je;
-        nxt = stream_item<MULTI, OSZ>(a, more ? j + G : j, more);
+        nxt = stream_item<MULTI, OSZ, NW>(a, more ? j + G : j, more);
     }
     // flush: the last item's last tile (P in pB, V in its slot: no refill has reached it)
     {
@@ -646,7 +676,8 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
     unsigned long long ck_exit[2];
     asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(ck_exit[0]), "=s"(ck_exit[1])::"memory");
     if (lane == 0 && a.stamps) {
-        unsigned long long* dst = a.stamps + ((size_t)blockIdx.x * kSW + wave) * 16;
+        unsigned long long* dst = a.stamps + ((size_t)blockIdx.x * NW + wave) * kStreamStampSlots;
+        for (int i_ = 0; i_ < 24; ++i_) dst[16 + i_] = sg[i_];
         for (int i_ = 0; i_ < 4; ++i_) dst[i_] = ck_sum[i_];
         dst[6] = ck_mid;
         dst[14] = ck_items;
@@ -660,23 +691,28 @@ __global__ __launch_bounds__(64 * kSW, 2) void mha_hd64_stream_kernel(FwdArgs a)
 }
 #undef MHA_SEL
 
-template <typename TOut>
+template <typename TOut, int NW>
 hipError_t launch_stream_t(const FwdArgs& a, int grid, hipStream_t stream) {
     if (a.n_calls > 1)
-        hipLaunchKernelGGL((mha_hd64_stream_kernel<TOut, true>), dim3(grid), dim3(64 * kSW), 0, stream, a);
+        hipLaunchKernelGGL((mha_hd64_stream_kernel<TOut, true, NW>), dim3(grid), dim3(64 * NW), 0, stream, a);
     else
-        hipLaunchKernelGGL((mha_hd64_stream_kernel<TOut, false>), dim3(grid), dim3(64 * kSW), 0, stream, a);
+        hipLaunchKernelGGL((mha_hd64_stream_kernel<TOut, false, NW>), dim3(grid), dim3(64 * NW), 0, stream, a);
     return hipGetLastError();
 }
 
 }  // namespace
 
-int stream_grid(int items, int /*waves*/) { return items < kSMaxGrid ? items : kSMaxGrid; }
+int stream_grid(int items, int waves) {
+    const int cap = waves == 8 ? stream_max_grid<8>() : stream_max_grid<4>();
+    return items < cap ? items : cap;
+}
 
-hipError_t launch_stream(const FwdArgs& a, int /*waves*/, bool out_f32, hipStream_t stream) {
-    const int grid = stream_grid(a.total_blocks, kSW);
+// waves: 4 (128-row items) or 8 (256-row items); a.total_blocks counts items of that size
+hipError_t launch_stream(const FwdArgs& a, int waves, bool out_f32, hipStream_t stream) {
+    const int grid = stream_grid(a.total_blocks, waves);
     if (grid <= 0) return hipSuccess;
-    return out_f32 ? launch_stream_t<float>(a, grid, stream) : launch_stream_t<f16>(a, grid, stream);
+    if (waves == 8) return out_f32 ? launch_stream_t<float, 8>(a, grid, stream) : launch_stream_t<f16, 8>(a, grid, stream);
+    return out_f32 ? launch_stream_t<float, 4>(a, grid, stream) : launch_stream_t<f16, 4>(a, grid, stream);
 }
 
 }  // namespace mha_hd64

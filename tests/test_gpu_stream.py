@@ -1,7 +1,7 @@
-"""Parity of the persistent streaming kernel (csrc/mha_hd64_stream.hip; forced plan code 23, or
-mha_hd64_set_stream_mode(1) for the planner) with the C oracle.
+"""Parity of the persistent streaming kernel (csrc/mha_hd64_stream.hip; forced plan code 23 with
+kv_waves 4 / 8 for its two forms, or mha_hd64_set_stream_mode(1) for the planner) with the C oracle.
 
-The kernel walks items (call, batch*head, 128-row block) with every key of the call per item; a
+The kernel walks items (call, batch*head, 128- or 256-row block) with every key of the call per item; a
 workgroup takes a contiguous range of items and its K/V ring runs on across item seams, so the
 cases below vary: items per workgroup (1 to 3; the grid is at most 512 workgroups), calls of
 different nkv in one launch (the MULTI form), partial last key tiles, one-tile items (nkv <= 64),
@@ -48,14 +48,14 @@ def _maxdiff(a, b):
     return float(np.abs(a.astype(np.float64) - b.astype(np.float64)).max())
 
 
-def _launch(lib, q, k, v, o, code=STREAM, ws=None):
+def _launch(lib, q, k, v, o, code=STREAM, ws=None, waves=0):
     from lightglue_amd import _lib
 
     b, h, nq, _ = q.shape
     nkv = k.shape[2]
     ws = ws if ws is not None else torch.empty(1 << 20, dtype=torch.uint8, device=q.device)
     st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), b, h, nq, nkv,
-                                    int(q.dtype == torch.float32), int(o.dtype == torch.float32), code, 0, 0,
+                                    int(q.dtype == torch.float32), int(o.dtype == torch.float32), code, waves, 0,
                                     ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream, 3)
     assert st == 0, _lib.last_error()
 
@@ -74,8 +74,9 @@ STREAM_SHAPES = [(1, 1, 1), (1, 100, 77), (1, 33, 65), (1, 129, 1), (1, 1000, 3)
                  (24, 1024, 1100), (36, 1000, 129)]
 
 
+@pytest.mark.parametrize("waves", [4, 8])
 @pytest.mark.parametrize("batch,nq,nkv", STREAM_SHAPES)
-def test_stream_kernel_matches_oracle(batch, nq, nkv, dev, oracle_mod):
+def test_stream_kernel_matches_oracle(batch, nq, nkv, waves, dev, oracle_mod):
     from lightglue_amd import _lib, synth
 
     lib = _lib.load()
@@ -87,15 +88,16 @@ def test_stream_kernel_matches_oracle(batch, nq, nkv, dev, oracle_mod):
     q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
     for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
         o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
-        _launch(lib, q, k, v, o)
+        _launch(lib, q, k, v, o, waves=waves)
         torch.cuda.synchronize()
         got = o.float().cpu().numpy()
         assert np.isfinite(got).all(), "unwritten or NaN output rows"
         d = _maxdiff(got[bsel][:, :, rows], ref)
-        assert d <= tol, (batch, nq, nkv, out_dt, d)
+        assert d <= tol, (batch, nq, nkv, waves, out_dt, d)
 
 
-def test_stream_kernel_running_max_moves(dev, oracle_mod):
+@pytest.mark.parametrize("waves", [4, 8])
+def test_stream_kernel_running_max_moves(waves, dev, oracle_mod):
     """A spike key moves a query's running max at the item's first tile (key 10), in a middle tile
     past the lazy-rescale threshold (key 300, gain 6), barely (gain 0.5: no rescale), and in the
     partial last tile (nkv 1100, key 1090); batch 40 gives every workgroup 2-3 items, so the
@@ -115,15 +117,16 @@ def test_stream_kernel_running_max_moves(dev, oracle_mod):
         q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
         for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
             o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
-            _launch(lib, q, k, v, o)
+            _launch(lib, q, k, v, o, waves=waves)
             torch.cuda.synchronize()
             got = o.float().cpu().numpy()
             assert np.isfinite(got).all()
             d = _maxdiff(got[bsel][:, :, rows], ref)
-            assert d <= tol, (nkv, krow, gain, out_dt, d)
+            assert d <= tol, (nkv, krow, gain, waves, out_dt, d)
 
 
-def test_stream_kernel_large_negative_logits(dev, oracle_mod):
+@pytest.mark.parametrize("waves", [4, 8])
+def test_stream_kernel_large_negative_logits(waves, dev, oracle_mod):
     """Scores far below zero everywhere (~ -200 raw, as test_gpu_parity.py's case) in a launch of
     several items per workgroup: each item's first tile must set its max (no underflow to l = 0).
     At this logit scale the fp16 operands of Q·Kᵀ alone put every plan ~6e-3 from the fp64 oracle
@@ -142,7 +145,7 @@ def test_stream_kernel_large_negative_logits(dev, oracle_mod):
     q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
     for out_dt in (torch.float16, torch.float32):
         o = torch.empty(q.shape, dtype=out_dt, device=dev)
-        _launch(lib, q, k, v, o)
+        _launch(lib, q, k, v, o, waves=waves)
         o2 = torch.empty(q.shape, dtype=out_dt, device=dev)
         _launch(lib, q, k, v, o2, code=0)
         torch.cuda.synchronize()
@@ -190,7 +193,8 @@ def test_stream_mode_grouped_calls(out_dt, tol, dev, oracle_mod, stream_mode):
     assert torch.equal(a, outs[0])  # one call alone: same items, same bits
 
 
-def test_stream_kernel_deterministic_and_capturable(dev):
+@pytest.mark.parametrize("waves", [4, 8])
+def test_stream_kernel_deterministic_and_capturable(waves, dev):
     from lightglue_amd import _lib, synth
 
     lib = _lib.load()
@@ -199,16 +203,16 @@ def test_stream_kernel_deterministic_and_capturable(dev):
     ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
     a = torch.empty_like(q)
     b = torch.empty_like(q)
-    _launch(lib, q, k, v, a, ws=ws)
-    _launch(lib, q, k, v, b, ws=ws)
+    _launch(lib, q, k, v, a, ws=ws, waves=waves)
+    _launch(lib, q, k, v, b, ws=ws, waves=waves)
     out = torch.empty_like(q)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     g = torch.cuda.CUDAGraph()
     with torch.cuda.stream(s):
-        _launch(lib, q, k, v, out, ws=ws)
+        _launch(lib, q, k, v, out, ws=ws, waves=waves)
         with torch.cuda.graph(g, stream=s):
-            _launch(lib, q, k, v, out, ws=ws)
+            _launch(lib, q, k, v, out, ws=ws, waves=waves)
     torch.cuda.current_stream().wait_stream(s)
     out.zero_()
     g.replay()
@@ -216,8 +220,9 @@ def test_stream_kernel_deterministic_and_capturable(dev):
     assert torch.equal(a, b) and torch.equal(out, a)
 
 
+@pytest.mark.parametrize("waves", [4, 8])
 @pytest.mark.parametrize("where", ["q", "k", "v"])
-def test_stream_kernel_nan_inputs(where, dev):
+def test_stream_kernel_nan_inputs(where, waves, dev):
     """NaNs reach the outputs the reference's PyTorch math gives them (a NaN query row -> that
     row; a NaN key row -> every row of the head; a NaN value element -> its column)."""
     from lightglue_amd import _lib, synth
@@ -233,9 +238,9 @@ def test_stream_kernel_nan_inputs(where, dev):
     q, k, v = (_t(a, dev, torch.float16) for a in (q16, k16, v16))
     for out_dt in (torch.float16, torch.float32):
         o = torch.empty(q.shape, dtype=out_dt, device=dev)
-        _launch(lib, q, k, v, o)
+        _launch(lib, q, k, v, o, waves=waves)
         torch.cuda.synchronize()
-        assert torch.equal(torch.isnan(o.float().cpu()), torch.isnan(ref)), (where, out_dt)
+        assert torch.equal(torch.isnan(o.float().cpu()), torch.isnan(ref)), (where, waves, out_dt)
 
 
 def test_stream_plan_reported_and_fp32_inputs_fall_back(dev, stream_mode):
@@ -250,7 +255,11 @@ def test_stream_plan_reported_and_fp32_inputs_fall_back(dev, stream_mode):
     lib.mha_hd64_plan(1, 4, 1024, 1024, 5242880, plan)
     assert plan[0] != STREAM  # 32 items: the single-pass kernel
     lib.mha_hd64_plan(16, 4, 1024, 1024, 5242880, plan)
-    assert plan[0] == STREAM
+    assert plan[0] == STREAM and plan[1] == 8  # 256 items of 256 rows: the 8-wave form
+    lib.mha_hd64_plan(12, 4, 1024, 1024, 5242880, plan)
+    assert plan[0] == STREAM and plan[1] == 8  # 192 of them: one round, 3/4 full
+    lib.mha_hd64_plan(24, 4, 1024, 1024, 5242880, plan)
+    assert plan[0] == STREAM and plan[1] == 4  # 384: a half-full second round -> 768 items of 128 rows
     stream_mode(0)
     lib.mha_hd64_plan(16, 4, 1024, 1024, 5242880, plan)
     assert plan[0] != STREAM

@@ -22,6 +22,9 @@ __device__ __forceinline__ void fill(float (&x)[16], int g) {
             x[r] = __builtin_bit_cast(float, h);
         }
         if (KIND == 3) x[r] = fmaxf(fmaxf(x[r], x[(r + 5) & 15]), x[(r + 9) & 15]);
+        if (KIND == 4) asm volatile("v_exp_f16 %0, %0" : "+v"(x[r]));  // (round 4: the half-precision exp)
+        if (KIND == 5) asm volatile("v_exp_f16_sdwa %0, %0 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0" : "+v"(x[r]));  // result to the high half (SDWA)
+        if (KIND == 6) asm volatile("v_exp_f32 %0, %0" : "+v"(x[r]));
     }
 }
 
@@ -102,6 +105,9 @@ int main() {
     for (int th : {256, 512}) {
         SWEEP(0, "exp", th);
         SWEEP(1, "add", th);
+        SWEEP(4, "exp_f16", th);
+        SWEEP(5, "exp_f16hi", th);
+        SWEEP(6, "exp_f32a", th);
     }
     return 0;
 }

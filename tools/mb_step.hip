@@ -20,6 +20,8 @@
 //           one step of DMA lead, as the round-3 streaming kernel) instead of the previous step's
 // NW = waves per workgroup: 4 (two workgroups per CU) or 8 (one per CU, two waves per SIMD sharing
 //           the K/V stream: 2 DMA pieces per wave and step)
+// 4096 ROT  (NW = 8) waves 4..7 run each step's phase B before its phase A: the two waves of a SIMD
+//           (w, w + 4) are in different phases between barriers
 // 512 POLY   half of the exponentials as a degree-3 exp2 polynomial on the
 //           packed-FMA path (v_pk_fma_f32 + exponent insert) instead of v_exp_f32
 // Prints per variant: µs per launch (HIP events, median of 5 launches), TFLOP/s (the step's useful
@@ -40,7 +42,7 @@
 using namespace mha_hd64;
 
 enum : int { EXP = 1, CVT = 2, MAX = 4, RSUM = 8, LDSK = 16, LDSV = 32, DMA = 64, BAR = 128, SCHK = 256, POLY = 512,
-              BAR2 = 1024, WAIT0 = 2048 };
+              BAR2 = 1024, WAIT0 = 2048, ROT = 4096 };
 constexpr int ITER = 1024;  // steps per wave (2 x this many tiles per loop trip)
 constexpr int kSlot = 2 * kTileBytes;
 constexpr int kSlots = 4;
@@ -213,6 +215,7 @@ __global__ __launch_bounds__(64 * NW, RB == 1 ? 2 : 1) void kern(const f16* src,
 
         int g = 0;
         // phase A: QKᵀ(t+1)
+        auto phase_a = [&](bool rv) {
         read_k(0);
         read_k(1);
         __builtin_amdgcn_sched_barrier(0);
@@ -226,14 +229,16 @@ __global__ __launch_bounds__(64 * NW, RB == 1 ? 2 : 1) void kern(const f16* src,
                     fill(g++);
                     if (b == 0 && kb == 0) {
                         if (s < 2) read_k(s + 2);
-                        if (s == 1) read_v(0);
-                        if (s == 2) read_v(1);
+                        if (rv && s == 1) read_v(0);
+                        if (rv && s == 2) read_v(1);
                         dma(s);
                     }
                     __builtin_amdgcn_sched_barrier(0);
                 }
         }
+        };
         // phase B: Oᵀ += Vᵀ·Pᵀ(t−1) and row sums
+        auto phase_b = [&]() {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int jj = k >> 1, ss = k & 1;
@@ -251,6 +256,16 @@ __global__ __launch_bounds__(64 * NW, RB == 1 ? 2 : 1) void kern(const f16* src,
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
+        }
+        };
+        if ((F & ROT) && wave >= NW / 2) {
+            read_v(0);  // (phase B first: its V fragments before it)
+            read_v(1);
+            phase_b();
+            phase_a(false);
+        } else {
+            phase_a(true);
+            phase_b();
         }
         while (g < G) fill(g++);  // (without RSUM: the remaining fillers after the last MFMA)
         asm volatile("" : "+v"(pn[0][0]), "+v"(pn[0][1]), "+v"(pn[0][2]), "+v"(pn[0][3]));
@@ -408,6 +423,9 @@ int main(int argc, char** argv) {
         row<1, 8, VECS | LDSK | LDSV | DMA | BAR>("j' 8 waves, sum check", filt, src, out, clk);
         row<1, 8, VECS | LDSK | LDSV | DMA | BAR | BAR2>("j2 8 waves, sum check, bar / 2", filt, src, out, clk);
         row<1, 8, VECS | LDSK | LDSV | DMA>("j3 8 waves, sum check, no bar", filt, src, out, clk);
+        row<1, 8, VEC | LDSK | LDSV | DMA | BAR | ROT>("k  8 waves, full step, rotated", filt, src, out, clk);
+        row<1, 8, VECS | LDSK | LDSV | DMA | BAR | ROT>("k' 8 waves, sum check, rotated", filt, src, out, clk);
+        row<1, 8, VECS | LDSK | LDSV | DMA | BAR | BAR2 | ROT>("k2 8 waves, sum check, bar / 2, rot", filt, src, out, clk);
     }
     return 0;
 }

@@ -34,11 +34,11 @@ def load(path):
     return lib
 
 
-def forced(lib, q, k, v, o, code, ws, stream):
+def forced(lib, q, k, v, o, code, ws, stream, kvw=0):
     b, h, nq, _ = q.shape
     nkv = k.shape[2]
     st = lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), b, h, nq, nkv,
-                                    int(q.dtype == torch.float32), int(o.dtype == torch.float32), code, 0, 0,
+                                    int(q.dtype == torch.float32), int(o.dtype == torch.float32), code, kvw, 0,
                                     ws.data_ptr(), ws.numel(), stream.cuda_stream, 3)
     if st != 0:
         raise RuntimeError(lib.mha_hd64_last_error().decode())
@@ -65,23 +65,20 @@ def parity(lib, dev, quick):
         ref = reference(q, k, v)
         row = {"shape": [b, 4, nq, nkv]}
         for od in (torch.float16, torch.float32):
-            o = torch.full(q.shape, float("nan"), dtype=od, device=dev)
-            forced(lib, q, k, v, o, STREAM, ws, stream)
-            o2 = torch.full(q.shape, float("nan"), dtype=od, device=dev)
-            forced(lib, q, k, v, o2, 0, ws, stream)
-            torch.cuda.synchronize()
-            row["f16out" if od == torch.float16 else "f32out"] = {
-                "max_abs_vs_fp32": float((o.float() - ref).abs().max()),
-                "planner_max_abs_vs_fp32": float((o2.float() - ref).abs().max()),
-                "nan": bool(torch.isnan(o).any()),
-            }
+            res = {}
+            for name, code, kvw in (("stream4", STREAM, 4), ("stream8", STREAM, 8), ("planner", 0, 0)):
+                o = torch.full(q.shape, float("nan"), dtype=od, device=dev)
+                forced(lib, q, k, v, o, code, ws, stream, kvw)
+                torch.cuda.synchronize()
+                res[name] = {"max_abs_vs_fp32": float((o.float() - ref).abs().max()), "nan": bool(torch.isnan(o).any())}
+            row["f16out" if od == torch.float16 else "f32out"] = res
         print(json.dumps(row), flush=True)
 
 
 def timing(lib, dev, quick):
     stream = torch.cuda.Stream()
     ws = torch.empty(5242880, dtype=torch.uint8, device=dev)
-    batches = (8, 16, 32) if not quick else (16,)
+    batches = (8, 12, 16, 24, 32, 64) if not quick else (16, 32)
     for B in batches:
         q = torch.randn(B, 4, 1024, 64, device=dev).half()
         k = torch.randn(B, 4, 1024, 64, device=dev).half()
@@ -89,13 +86,13 @@ def timing(lib, dev, quick):
         o = torch.empty_like(q)
         K = max(20, 400 // B)
         graphs = {}
-        for name, code in (("stream", STREAM), ("planner", 0)):
+        for name, code, kvw in (("stream4", STREAM, 4), ("stream8", STREAM, 8), ("ring", 4, 1), ("planner", 0, 0)):
             with torch.cuda.stream(stream):
-                forced(lib, q, k, v, o, code, ws, stream)  # warm, plan
+                forced(lib, q, k, v, o, code, ws, stream, kvw)  # warm, plan
                 gr = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(gr, stream=stream):
                     for _ in range(K):
-                        forced(lib, q, k, v, o, code, ws, stream)
+                        forced(lib, q, k, v, o, code, ws, stream, kvw)
             graphs[name] = gr
         torch.cuda.synchronize()
         times = {n: [] for n in graphs}

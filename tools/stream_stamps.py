@@ -1,6 +1,6 @@
 """Diagnostic: where a step of the persistent streaming kernel spends its cycles, from a
 -DMHA_STREAM_STAMPS build (tools/build_stream_variant.sh stamps -DMHA_STREAM_STAMPS).
-    python tools/stream_stamps.py <lib.so> [batch] [nq] [nkv]
+    [STREAM_WAVES=8] python tools/stream_stamps.py <lib.so> [batch] [nq] [nkv]
 Per wave: s_memtime cycles per step by segment (refill issue, decision/seam, phase A issue,
 phase B issue, DMA wait, barrier), medians and p90 over waves, steps per wave, the in-kernel clock
 (s_memtime / s_memrealtime) and the share of a wave's life spent in steps."""
@@ -19,6 +19,7 @@ from lightglue_amd import _lib  # noqa: E402
 _lib.LIB_PATH = os.path.abspath(sys.argv[1])
 lib = _lib.load()
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 32
+W = int(os.environ.get("STREAM_WAVES", "4"))  # forced plan 23 with kv_waves 4 / 8
 nq = int(sys.argv[3]) if len(sys.argv) > 3 else 1024
 nkv = int(sys.argv[4]) if len(sys.argv) > 4 else 1024
 dev = torch.device("cuda:0")
@@ -27,17 +28,16 @@ k = torch.randn(B, 4, nkv, 64, device=dev).half()
 v = torch.randn(B, 4, nkv, 64, device=dev).half()
 o = torch.empty_like(q)
 ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
-st = torch.zeros(512 * 8 * 16, dtype=torch.int64, device=dev)
+st = torch.zeros(512 * 8 * 48, dtype=torch.int64, device=dev)
 lib.mha_hd64_set_stamp_buffer(st.data_ptr())
 s = torch.cuda.current_stream().cuda_stream
 for _ in range(20):
     assert lib.mha_hd64_launch_forced(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), B, 4, nq, nkv, 0, 0, 23,
-                                      0, 0, ws.data_ptr(), ws.numel(), s, 3) == 0
+                                      W, 0, ws.data_ptr(), ws.numel(), s, 3) == 0
 torch.cuda.synchronize()
-W = int(os.environ.get("MHA_HD64_STREAM_WAVES", "4"))
 items = B * 4 * -(-nq // (32 * W))
 grid = min(items, 512 if W == 4 else 256)
-t = st[: grid * W * 16].view(grid * W, 16).cpu().numpy().astype(np.float64)
+t = st[: grid * W * 48].view(grid * W, 48).cpu().numpy().astype(np.float64)
 # layout (csrc/mha_hd64_stream.hip, MHA_STREAM_STAMPS): 0 the first item's tile 0 (kernel
 # prologue), 1 first steps, 2 middle loop, 3 tail + last steps + epilogues, 6 middle steps, 14
 # items, 8..11 entry / exit clocks, 12 end of the kernel prologue's loads
@@ -73,4 +73,14 @@ out["life_us_by_xcd"] = [round(float(np.median(real[wg % 8 == x])), 2) for x in 
 out["clock_ghz_by_xcd"] = [round(float(np.median(clk[wg % 8 == x])), 3) for x in range(8)]
 out["life_us_by_half"] = [round(float(np.median(real[wg < grid // 2])), 2), round(float(np.median(real[wg >= grid // 2])), 2)]
 out["middle_cyc_by_xcd"] = [round(float(np.median((t[:, 2] / nmid)[wg % 8 == x])), 1) for x in range(8)]
+# chained segments (cycles per item, per middle step)
+names = ["item_advance", "next_q_issue", "first_A", "first_B", "first_epi_wait", "first_barrier", "mid_A", "mid_B",
+         "mid_wait", "mid_barrier", "tail_A", "tail_B", "tail_wait", "tail_barrier", "to_last", "read_q", "last_A",
+         "last_B", "last_wait", "last_barrier"]
+seg = {}
+for k, nm in enumerate(names):
+    col = t[:, 16 + k]
+    den = nmid if nm.startswith("mid") else items
+    seg[nm] = round(float(np.median(col / den)), 1)
+out["segments"] = seg
 print(json.dumps(out))
