@@ -294,6 +294,18 @@ __device__ __forceinline__ void lds_dma16(unsigned m0, unsigned voff, __amdgpu_b
         : "v"(voff), "s"(rs), "s"(soff), "{m0}"(m0)
         : "memory");
 }
+// The same with one wait state, for call sites whose M0, soffset and descriptor are SALU values
+// (a SALU write of M0 needs 1 wait state before an LDS-DMA load; no VALU writes them): the hot
+// refill of the streaming kernel. tools/check_dma_hazards.py audits every LDS-DMA load of the
+// built library against both rules (tests/test_abi.py runs it).
+__device__ __forceinline__ void lds_dma16_s(unsigned m0, unsigned voff, __amdgpu_buffer_rsrc_t rs, unsigned soff) {
+    asm volatile(
+        "s_nop 0\n\t"
+        "buffer_load_dwordx4 %0, %1, %2 offen lds"
+        :
+        : "v"(voff), "s"(rs), "s"(soff), "{m0}"(m0)
+        : "memory");
+}
 // LDS byte address of a pointer into a __shared__ array (the value M0 takes)
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
     return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;

@@ -90,11 +90,18 @@ namespace {
 // K/V tile, one workgroup per CU)
 template <int NW>
 constexpr int stream_rows() { return 32 * NW; }  // query rows per item
-constexpr int kSSlot = 2 * kTileBytes;         // one ring slot: K image, then V image (16 KiB)
-constexpr int kSSlots = 4;                     // ring slots
-constexpr int kSQOff = kSSlots * kSSlot;       // Q region: the item's rows (16 / 32 KiB)
+constexpr int kSSlot = 2 * kTileBytes;            // one ring slot: K image, then V image (16 KiB)
+// ring slots and lead (the refill of step t is global tile t + lead): NW 4: 4 slots, lead 2, a
+// barrier every step (80 KiB: two workgroups per CU); NW 8: 8 slots, lead 4, a barrier every second
+// step (160 KiB, the whole LDS)
 template <int NW>
-constexpr int stream_lds() { return kSQOff + stream_rows<NW>() * 128; }  // 80 KiB (NW 4) / 96 KiB (NW 8)
+constexpr int stream_slots() { return NW == 8 ? 8 : 4; }
+template <int NW>
+constexpr int stream_lead() { return NW == 8 ? 4 : 2; }
+template <int NW>
+constexpr int stream_q_off() { return stream_slots<NW>() * kSSlot; }  // Q region: the item's rows
+template <int NW>
+constexpr int stream_lds() { return stream_q_off<NW>() + stream_rows<NW>() * 128; }  // 80 / 160 KiB
 template <int NW>
 constexpr int stream_max_grid() { return NW == 4 ? 512 : 256; }  // one residency round
 
@@ -127,13 +134,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t stream_rsrc(const void* base, 
     return make_rsrc((const void*)(((unsigned long long)hi << 32) | lo), __builtin_amdgcn_readfirstlane(bytes));
 }
 
-// One item's scalar description (batch·head offsets applied) and its K/V / Q / O descriptors.
+// One item's scalar description for the compute side (batch·head offsets applied): its Q and O
+// descriptors, key count, first query row and tile count.
 struct StreamItem {
-    __amdgpu_buffer_rsrc_t k, v, q, o;
+    __amdgpu_buffer_rsrc_t q, o;
     int nkv;
     int q0;  // first query row of the block
     int nt;  // 64-key tiles, rounded up to an even count (the padding tile reads zeros, masked)
 };
+// The loader's cursor: K/V descriptors of the item whose tiles it issues, its next local tile, its
+// tile count and its index. It runs `lead` tiles ahead of the compute side, across item seams
+// (over several short items if need be).
+struct StreamLoader {
+    __amdgpu_buffer_rsrc_t k, v;
+    int lt, nt, j;
+};
+
+__device__ __forceinline__ int stream_tiles(int nkv) { return ((nkv + 2 * kTileKV - 1) / (2 * kTileKV)) * 2; }
 
 template <bool MULTI, int OSZ, int NW>
 __device__ __forceinline__ StreamItem stream_item(const FwdArgs& a, int j, bool live) {
@@ -141,25 +158,15 @@ __device__ __forceinline__ StreamItem stream_item(const FwdArgs& a, int j, bool 
     const int nq = MHA_SEL(nq), nkv = MHA_SEL(nkv), qtiles = MHA_SEL(qtiles);
     const int jl = j - MHA_SEL(block_begin);
     const int bh = jl / qtiles, qtile = jl - bh * qtiles;
-#ifdef MHA_STREAM_L2KV  // diagnostic: every item streams the first head's K/V (L2-resident)
-    const int bhk = 0;
-#else
-    const int bhk = bh;
-#endif
 #ifdef MHA_STREAM_L2Q  // diagnostic: every item reads the first query block (L2-resident)
     const int bhq = 0;
 #else
     const int bhq = bh;
 #endif
     const char* q = reinterpret_cast<const char*>(MHA_SEL(q)) + (size_t)bhq * nq * (kHeadDim * 2);
-    const char* k = reinterpret_cast<const char*>(MHA_SEL(k)) + (size_t)bhk * nkv * (kHeadDim * 2);
-    const char* v = reinterpret_cast<const char*>(MHA_SEL(v)) + (size_t)bhk * nkv * (kHeadDim * 2);
     char* o = reinterpret_cast<char*>(MHA_SEL(o)) + (size_t)bh * nq * (kHeadDim * OSZ);
     StreamItem it;
-    // (a dead item — past the workgroup's last — gets empty descriptors: its DMA pieces read zeros)
-    const unsigned kvb = live ? (unsigned)nkv * kHeadDim * 2 : 0u;
-    it.k = stream_rsrc(k, kvb);
-    it.v = stream_rsrc(v, kvb);
+    // (a dead item — past the workgroup's last — gets an empty Q descriptor: its DMA reads zeros)
     it.q = stream_rsrc(q, live ? (unsigned)nq * kHeadDim * 2 : 0u);
     it.o = stream_rsrc(o, (unsigned)nq * kHeadDim * OSZ);
     it.nkv = nkv;
@@ -168,8 +175,31 @@ __device__ __forceinline__ StreamItem stream_item(const FwdArgs& a, int j, bool 
 #else
     it.q0 = qtile * stream_rows<NW>();
 #endif
-    it.nt = ((nkv + 2 * kTileKV - 1) / (2 * kTileKV)) * 2;
+    it.nt = stream_tiles(nkv);
     return it;
+}
+
+template <bool MULTI>
+__device__ __forceinline__ StreamLoader stream_kv(const FwdArgs& a, int j, bool live) {
+    const int ci = stream_call<MULTI>(a, j);
+    const int nkv = MHA_SEL(nkv), qtiles = MHA_SEL(qtiles);
+    const int bh = (j - MHA_SEL(block_begin)) / qtiles;
+#ifdef MHA_STREAM_L2KV  // diagnostic: every item streams the first head's K/V (L2-resident)
+    const int bhk = 0;
+#else
+    const int bhk = bh;
+#endif
+    const char* k = reinterpret_cast<const char*>(MHA_SEL(k)) + (size_t)bhk * nkv * (kHeadDim * 2);
+    const char* v = reinterpret_cast<const char*>(MHA_SEL(v)) + (size_t)bhk * nkv * (kHeadDim * 2);
+    StreamLoader ld;
+    // (past the workgroup's last item: empty descriptors, zeros into the ring, forever)
+    const unsigned kvb = live ? (unsigned)nkv * kHeadDim * 2 : 0u;
+    ld.k = stream_rsrc(k, kvb);
+    ld.v = stream_rsrc(v, kvb);
+    ld.lt = 0;
+    ld.nt = live ? stream_tiles(nkv) : (1 << 30);
+    ld.j = j;
+    return ld;
 }
 
 // fp16 Q scaled by 0.125·log2(e): each half rounded once from the fp32 product (v_fma_mix), the
@@ -200,6 +230,9 @@ template <typename TOut, bool MULTI, int NW>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kernel(FwdArgs a) {
     constexpr int OSZ = (int)sizeof(TOut);
     constexpr int kPW = 8 / NW;  // DMA pieces (1 KiB, 8 rows) per wave of each 8 KiB K or V image
+    constexpr int kPiece = 2 * kPW;  // DMA pieces per wave and tile (K and V)
+    constexpr unsigned kSM = (unsigned)stream_slots<NW>() - 1u;  // ring slot = global tile & kSM
+    constexpr int L = stream_lead<NW>();  // the refill of step t: global tile t + L
     __shared__ __attribute__((aligned(1024))) char smem[stream_lds<NW>()];
     lds_char* const lds = (lds_char*)smem;
     const unsigned lds0 = (unsigned)(uintptr_t)lds;
@@ -236,7 +269,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
     unsigned k_addr[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) k_addr[s] = (unsigned)k_off(r, 2 * s + hh);
-    const unsigned q_base = (unsigned)(kSQOff + 32 * wave * 128);
+    const unsigned q_base = (unsigned)(stream_q_off<NW>() + 32 * wave * 128);
     // V image (A operand of Oᵀ = Vᵀ·Pᵀ via ds_read_b64_tr_b16): as the LDS-ring kernel's.
     const int g16 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
     const int vb = (qq >> 1) & 1;
@@ -258,15 +291,25 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
     const f16 sel = (((lane & 15) >> 2) & 1) == ((lane >> 4) & 1) ? (f16)1.f : (f16)0.f;
     const f16x8 a_sum = f16x8{sel, sel, sel, sel, sel, sel, sel, sel};
 
-    // K and V pieces of local tile lt of an item into ring slot `slot`
-    auto issue_tile = [&](const StreamItem& it, int lt, unsigned slot) {
+    // The loader's K and V pieces of its current tile into ring slot `slot` (pieces wave + NW·h of
+    // each image, 8 KiB apart per image), then its cursor moves on (past an item's last tile: the
+    // workgroup's next item, or an empty one past the last)
+    StreamLoader ld = stream_kv<MULTI>(a, j, true);
+    auto issue_tile = [&](unsigned slot) {
         const unsigned m = m0w + slot * (unsigned)kSSlot;
-        const unsigned so = (unsigned)lt * (unsigned)kTileBytes + sow;
+        const unsigned so = (unsigned)ld.lt * (unsigned)kTileBytes + sow;
 #pragma unroll
-        for (int h = 0; h < kPW; ++h) {  // pieces wave + NW·h of each image (8 KiB apart per image)
+        for (int h = 0; h < kPW; ++h) {
             const unsigned ho = (unsigned)(h * NW * 1024);
-            lds_dma16(m + ho, dma_k, it.k, so + ho);
-            lds_dma16(m + (unsigned)kTileBytes + ho, dma_v, it.v, so + ho);
+            lds_dma16(m + ho, dma_k, ld.k, so + ho);
+            lds_dma16(m + (unsigned)kTileBytes + ho, dma_v, ld.v, so + ho);
+        }
+    };
+    auto ld_advance = [&]() {
+        if (++ld.lt >= ld.nt) {  // (wave-uniform, once per item)
+            const int jn = ld.j + G;
+            ld = stream_kv<MULTI>(a, jn < je ? jn : ld.j, jn < je);
+            ld.j = jn;
         }
     };
     // this wave's 32 Q rows of an item into its part of the Q region
@@ -280,7 +323,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
     // ---- state ----
     StreamItem cur = stream_item<MULTI, OSZ, NW>(a, j, true);
     StreamItem nxt = stream_item<MULTI, OSZ, NW>(a, j + G < je ? j + G : j, j + G < je);
-    unsigned gb = 0;  // global tile index of the current item's tile 0 (ring slot = index mod 4)
+    unsigned gb = 0;  // global tile index of the current item's tile 0 (ring slot = index & kSM)
     f16x8 qf[4];
     f32x16 cm;                  // −m (the QKᵀ chains' C operand)
     f32x16 o0, o1;              // Oᵀ: dims 0..31 / 32..63, query on the lane
@@ -288,19 +331,24 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
     StreamScores sA, sB;
     f16x8 pA[2][2], pB[2][2];   // P (fp16) of a tile: B operand of k-step (jj, ss) of Oᵀ = Vᵀ·Pᵀ
 
-    // kernel prologue: the first item's Q and tiles 0, 1 landed everywhere; the V image of slot 3
-    // and pB zeroed: the first FIRST step's P·V of "tile −1" adds 0·0
+    // kernel prologue: the first item's Q and global tiles 0 .. L − 1 issued; Q and tiles 0, 1
+    // landed everywhere (NW 8: tiles 2, 3 stay in flight; the first item's FIRST step waits for
+    // tile 2 before its barrier); the V image of the last slot and pB zeroed: the first FIRST step's
+    // P·V of "tile −1" adds 0·0 (that slot's first refill is tile kSM, issued after a barrier)
     issue_q(cur);
-    issue_tile(cur, 0, 0u);
-    issue_tile(cur, 1, 1u);
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+        issue_tile((unsigned)i);
+        ld_advance();
+    }
 #pragma unroll
     for (unsigned off = (unsigned)tid * 16u; off < (unsigned)kTileBytes; off += 64u * NW * 16u)
-        lds_write16(lds, 3u * (unsigned)kSSlot + (unsigned)kTileBytes + off, f16x8{});
+        lds_write16(lds, kSM * (unsigned)kSSlot + (unsigned)kTileBytes + off, f16x8{});
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) pB[jj][ss] = f16x8{};
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 2) * kPiece) : "memory");
     __builtin_amdgcn_s_barrier();
 #ifdef MHA_STREAM_STAMPS
     SCLK(ck_pro);
@@ -378,19 +426,18 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
     __amdgpu_buffer_rsrc_t prv_o = cur.o;
     int prv_q0 = 0;
     unsigned qbad_prv = 0;
-    // The output stores of one epilogue (16 B each): the FIRST step issues them after its refill,
-    // so its counted wait leaves exactly these in flight
-    constexpr int kEpiStores = OSZ == 2 ? 4 : 8;
 
     // One step of the current item — every step is a full step of the pipeline: tile t's
     // exponentials; QKᵀ of global tile g + 1 (LAST: the next item's tile 0, with the next item's Q
     // and C = 0); P·V of global tile g − 1 (FIRST: the previous item's last tile, then that item's
     // epilogue — unless PREV is false: the workgroup's first item); the refill of global tile
-    // g + 2; the step's counted wait + barrier. MASK: tile t + 1 may hold keys past nkv. c: scores
-    // of tile t; n: of tile t + 1; pp: P of tile g − 1 (consumed); pn: P of tile t (produced).
-    // One instantiation per kind (KIND: 0 FIRST, 1 MIDDLE, 2 TAIL, 3 LAST), each called from one
-    // place: step variants in the arms of a branch would share their first instructions, which
-    // the IR passes hoist above the branch — the whole exponential block, out of the interleave.
+    // g + L (the loader's cursor); the step's counted wait + barrier (NW 8: odd steps only; nt is
+    // even, so every item starts on an even global tile). MASK: tile t + 1 may hold keys past nkv.
+    // c: scores of tile t; n: of tile t + 1; pp: P of tile g − 1 (consumed); pn: P of tile t
+    // (produced). One instantiation per kind (KIND: 0 FIRST, 1 / 4 MIDDLE odd / even t, 2 / 5 TAIL
+    // odd / even t, 3 LAST), each called from one place: step variants in the arms of a branch
+    // would share their first instructions, which the IR passes hoist above the branch — the whole
+    // exponential block, out of the interleave.
     // FIRST always runs its P·V (the workgroup's first item: P = 0 against a zeroed V image) and
     // decides at run time whether an epilogue follows; TAIL and LAST mask at run time.
     auto step = [&](auto kind_c, int t, StreamScores& c, StreamScores& n, const f16x8 (&pp)[2][2],
@@ -399,10 +446,17 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         constexpr bool FIRST = KIND == 0;
         constexpr bool PV = true;  // a P·V of global tile g − 1 in phase B
         constexpr bool LAST = KIND == 3;
-        constexpr bool MASK = KIND == 0 || KIND >= 2;  // tile t + 1 may hold keys past nkv
+        constexpr bool MASK = KIND == 0 || KIND == 2 || KIND == 3 || KIND == 5;  // tile t + 1 may hold keys past nkv
+        constexpr bool BAR = NW == 4 || KIND == 1 || KIND == 2 || KIND == 3;  // (NW 8: odd t)
         const unsigned g = gb + (unsigned)t;
-        const unsigned kbase = ((g + 1u) & 3u) * (unsigned)kSSlot;  // K of tile t + 1
-        const unsigned vbase = ((g - 1u) & 3u) * (unsigned)kSSlot;  // V of tile t − 1
+#ifdef MHA_STREAM_PRIO_BAL
+        // NW 8, between two barriers: the first step at raised priority, the second at normal, so
+        // the wave of a SIMD pair that finishes its first step ahead (the older one, on age) yields
+        // the issue to the other until it catches up (experiment)
+        if constexpr (NW == 8) __builtin_amdgcn_s_setprio(BAR ? 0 : 1);
+#endif
+        const unsigned kbase = ((g + 1u) & kSM) * (unsigned)kSSlot;  // K of tile t + 1
+        const unsigned vbase = ((g - 1u) & kSM) * (unsigned)kSSlot;  // V of tile t − 1
         // FIRST: tile 0's scores came from a C = 0 chain (the previous item's last step, or the
         // kernel prologue); its exact row max becomes the item's running max
         if constexpr (FIRST) {
@@ -423,17 +477,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
             c.s0 -= d;
             c.s1 -= d;
         }
-        // the refill: tile t + 2 of this item, or (last two steps) tile t + 2 − nt of the next
-        const bool own = t + 2 < cur.nt;
-        const int lt = own ? t + 2 : t + 2 - cur.nt;
-        const __amdgpu_buffer_rsrc_t rk_ = own ? cur.k : nxt.k;
-        const __amdgpu_buffer_rsrc_t rv_ = own ? cur.v : nxt.v;
-        const unsigned fm = m0w + ((g + 2u) & 3u) * (unsigned)kSSlot;
-        const unsigned fso = (unsigned)lt * (unsigned)kTileBytes + sow;
+        // the refill: global tile g + L, the loader's current tile (of this item or a later one)
+        const __amdgpu_buffer_rsrc_t rk_ = ld.k;
+        const __amdgpu_buffer_rsrc_t rv_ = ld.v;
+        const unsigned fm = m0w + ((g + (unsigned)L) & kSM) * (unsigned)kSSlot;
+        const unsigned fso = (unsigned)ld.lt * (unsigned)kTileBytes + sow;
         auto dma = [&](int i) {  // piece i (< 2 kPW) of the refill: K w, (K w+4,) V w(, V w+4)
             const unsigned ho = (unsigned)((i % kPW) * NW * 1024);
-            if (i < kPW) lds_dma16(fm + ho, dma_k, rk_, fso + ho);
-            else lds_dma16(fm + (unsigned)kTileBytes + ho, dma_v, rv_, fso + ho);
+            if (i < kPW) lds_dma16_s(fm + ho, dma_k, rk_, fso + ho);
+            else lds_dma16_s(fm + (unsigned)kTileBytes + ho, dma_v, rv_, fso + ho);
         };
 
         // ---- vector work, a fixed order over the step's MFMA gaps ----
@@ -475,7 +527,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
             if (gi >= 14 && gi < 18) maxk(gi - 14);
         };
 
-        constexpr int SB = KIND == 0 ? 2 : KIND == 1 ? 6 : KIND == 2 ? 10 : 16;  // (stamps: segment base)
+        constexpr int SB = KIND == 0 ? 2 : (KIND == 1 || KIND == 4) ? 6 : (KIND == 2 || KIND == 5) ? 10 : 16;  // (stamps)
         int gi = 0;
         // phase A: QKᵀ(t + 1), each gap an exponential pair (+ LDS reads, DMA pieces, packs). In
         // the LAST step, tile t + 1 is the next item's tile 0 (global tile g + 1, landed two
@@ -543,30 +595,41 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
             l_acc *= alpha;
         }
         if constexpr (FIRST) {  // the previous item is complete: its output, then a fresh O and l
-            if (prev) {
-                epilogue(prv_o, prv_q0, qbad_prv);
-                // the refill has landed (every VMEM op of this wave but the epilogue's stores,
-                // issued after it)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kEpiStores) : "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+            if (prev) epilogue(prv_o, prv_q0, qbad_prv);
             o0 = f32x16{};
             o1 = f32x16{};
             l_acc = f32x4{0.f, 0.f, 0.f, 0.f};
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the refill has landed
         }
         SEG(SB + 2);
-        // ... then every wave's
-        __builtin_amdgcn_s_barrier();
+        // The step's wait and barrier. Loads (LDS-DMA pieces) complete in issue order; a count
+        // below never lets an older store or Q piece stay in flight.
+        if constexpr (NW == 4) {
+            // this step's refill (tile t + 2, whose K the next step reads) has landed everywhere;
+            // FIRST: the epilogue's stores and the next item's Q pieces too
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        } else if constexpr (BAR) {
+            // (odd t) every refill up to the previous step's has landed (tiles up to t + 3: the K
+            // read in the next two steps); this step's tile t + 4 stays in flight
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kPiece) : "memory");
+            __builtin_amdgcn_s_barrier();
+        } else if constexpr (FIRST) {
+            if (!prev) {  // the workgroup's first item: the prologue's tile 2 is read next step
+                // (in flight: the prologue's tile 3, the next item's Q pieces, this step's tile 4)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kPiece + 4) : "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+        }
         SEG(SB + 3);
+        ld_advance();
     };
 
     using K0 = std::integral_constant<int, 0>;
     using K1 = std::integral_constant<int, 1>;
     using K2 = std::integral_constant<int, 2>;
     using K3 = std::integral_constant<int, 3>;
+    using K4 = std::integral_constant<int, 4>;
+    using K5 = std::integral_constant<int, 5>;
     // Q fragments of an item's rows from the Q region (this wave's own rows: its own DMA, waited at
     // a step's end), scaled; the mask of non-finite query rows
     auto read_q = [&]() -> unsigned {
@@ -617,7 +680,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         int t = 1;
         for (; t + 2 < nt && t + 2 < nfull; t += 2) {
             step(K1{}, t, sB, sA, pA, pB);
-            step(K1{}, t + 1, sA, sB, pB, pA);
+            step(K4{}, t + 1, sA, sB, pB, pA);
         }
 #ifdef MHA_STREAM_STAMPS
         SCLK(ck_t1);
@@ -628,7 +691,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         // the tail pairs: tiles past the full ones masked
         for (; t + 2 < nt; t += 2) {
             step(K2{}, t, sB, sA, pA, pB);
-            step(K2{}, t + 1, sA, sB, pB, pA);
+            step(K5{}, t + 1, sA, sB, pB, pA);
         }
         // the last step: beside tile nt − 2's P·V, the next item's tile 0 (its Q first: the
         // current item's fragments are no longer needed); tile nt − 1's P·V and this item's
@@ -658,7 +721,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
     }
     // flush: the last item's last tile (P in pB, V in its slot: no refill has reached it)
     {
-        const unsigned vb_t = ((gb + (unsigned)cur.nt - 1u) & 3u) * (unsigned)kSSlot;
+        const unsigned vb_t = ((gb + (unsigned)cur.nt - 1u) & kSM) * (unsigned)kSSlot;
         read_v(vb_t, 0);
         read_v(vb_t, 1);
 #pragma unroll

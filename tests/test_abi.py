@@ -337,3 +337,41 @@ def test_planner_invariants_fuzzed(lib):
         half = lib.mha_hd64_launch_workspace_bytes_typed(b, h, nq, nkv, 1)
         assert half == lib.mha_hd64_launch_workspace_bytes(b, h, nq, nkv)
         assert lib.mha_hd64_launch_workspace_bytes_typed(b, h, nq, nkv, 0) >= 0
+
+
+def _dma_checker():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("check_dma_hazards", os.path.join(REPO, "tools", "check_dma_hazards.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_dma_hazard_rules_on_synthetic_sequences():
+    """tools/check_dma_hazards.py flags a VALU write of an LDS-DMA load's SGPR operand (soffset,
+    descriptor, M0) fewer than 5 wait states before it and a SALU write of M0 right before it."""
+    c = _dma_checker()
+
+    def seq(*ins):
+        return [("k", [(op, dst, src) for op, dst, src in ins])]
+
+    load = ("buffer_load_dwordx4", "v1", " s[8:11], s4 offen lds")
+    assert c.check(seq(("v_readfirstlane_b32", "s4", " v2"), ("s_nop", "0", ""), load)) == (1, 1)
+    assert c.check(seq(("v_readfirstlane_b32", "s4", " v2"), ("s_nop", "4", ""), load)) == (1, 0)
+    assert c.check(seq(("v_readfirstlane_b32", "s9", " v2"), ("s_add_i32", "s5", " s5, 1"), load)) == (1, 1)
+    assert c.check(seq(("s_mov_b32", "m0", " s3"), load)) == (1, 1)
+    assert c.check(seq(("s_mov_b32", "m0", " s3"), ("s_nop", "0", ""), load)) == (1, 0)
+    assert c.check(seq(("v_readfirstlane_b32", "s3", " v2"), ("s_mov_b32", "m0", " s3"), ("s_nop", "0", ""), load)) == (1, 0)
+
+
+def test_built_library_dma_wait_states():
+    """Every LDS-DMA load of the built gfx950 code objects keeps the wait states (inline asm: the
+    compiler's hazard recognizer does not see inside it)."""
+    import shutil
+
+    if not shutil.which("objcopy") or not os.path.exists(os.path.join("/opt/rocm", "lib", "llvm", "bin", "llvm-objdump")):
+        pytest.skip("needs objcopy and the ROCm llvm-objdump")
+    c = _dma_checker()
+    checked, bad = c.check(c.parse(c.disassemble(c.DEFAULT_LIB)))
+    assert checked > 1000 and bad == 0, (checked, bad)

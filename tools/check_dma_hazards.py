@@ -1,0 +1,121 @@
+"""Audit the LDS-DMA issue sequences of the built library (gfx950 wait-state rules the compiler's
+hazard recognizer does not apply inside inline asm).
+
+For every `buffer_load_dword* ... lds` in the final code object, walk back over the instructions
+before it (straight-line, in emission order) and check:
+  * a VALU instruction that writes an SGPR the load reads (its descriptor, its soffset, M0) needs
+    5 wait states before the load;
+  * a SALU write of M0 needs 1 wait state before an LDS-DMA load.
+Wait states: every instruction counts 1, `s_nop N` counts N + 1.
+
+    python tools/check_dma_hazards.py [lib/libmha_hd64.so]
+Exit status 1 on a violation. Needs objcopy, clang-offload-bundler and llvm-objdump (ROCm).
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+LLVM = os.path.join(ROCM, "lib", "llvm", "bin")
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEFAULT_LIB = os.path.join(REPO, "lightglue-with-flashattentionv2-tensorrt_amd", "lib", "libmha_hd64.so")
+
+
+def disassemble(lib):
+    """The .hip_fatbin section holds one offload bundle per translation unit: unbundle each."""
+    lines = []
+    with tempfile.TemporaryDirectory() as d:
+        fat = os.path.join(d, "fat.bundle")
+        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", lib], check=True, capture_output=True)
+        data = open(fat, "rb").read()
+        magic = b"__CLANG_OFFLOAD_BUNDLE__"
+        starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+        for n, (a, b) in enumerate(zip(starts, starts[1:] + [len(data)])):
+            part, co = os.path.join(d, f"b{n}.bundle"), os.path.join(d, f"b{n}.co")
+            open(part, "wb").write(data[a:b])
+            r = subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o",
+                                f"--input={part}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"],
+                               capture_output=True)
+            if r.returncode != 0 or not os.path.getsize(co):
+                continue
+            out = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", co], check=True,
+                                 capture_output=True, text=True).stdout
+            lines += out.splitlines()
+    return lines
+
+
+def sgprs(text):
+    out = set()
+    for m in re.finditer(r"\bs\[(\d+):(\d+)\]", text):
+        out.update(f"s{i}" for i in range(int(m.group(1)), int(m.group(2)) + 1))
+    for m in re.finditer(r"\bs(\d+)\b", text):
+        out.add(f"s{m.group(1)}")
+    if re.search(r"\bm0\b", text):
+        out.add("m0")
+    return out
+
+
+def parse(lines):
+    """-> list of (function, [(op, dst_text, src_text)])"""
+    funcs, cur, name = [], [], None
+    for raw in lines:
+        m = re.match(r"^[0-9a-f]+ <(.+)>:", raw)
+        if m:
+            if name is not None:
+                funcs.append((name, cur))
+            name, cur = m.group(1), []
+            continue
+        s = raw.strip()
+        if not s or s.startswith(";") or s.endswith(">:") or ":" in s.split()[0]:
+            continue
+        s = s.split("//")[0].strip()
+        parts = s.split(None, 1)
+        op = parts[0]
+        args = parts[1] if len(parts) > 1 else ""
+        dst, _, src = args.partition(",")
+        cur.append((op, dst.strip(), src))
+    if name is not None:
+        funcs.append((name, cur))
+    return funcs
+
+
+def check(funcs):
+    bad = checked = 0
+    for name, ins in funcs:
+        for i, (op, dst, src) in enumerate(ins):
+            if not (op.startswith("buffer_load_dword") and " lds" in (dst + "," + src) + " "):
+                if not (op.startswith("buffer_load_dword") and src.rstrip().endswith("lds")):
+                    continue
+            checked += 1
+            reads = sgprs(src) | {"m0"}
+            ws = 0  # wait states between instruction j and the load
+            for j in range(i - 1, max(-1, i - 12), -1):
+                pop, pdst, _ = ins[j]
+                written = sgprs(pdst) if not pop.startswith(("s_nop", "s_waitcnt", "s_barrier", "buffer_", "ds_", "s_cbranch", "s_branch")) else set()
+                if pop.startswith("v_") and written & reads and ws < 5:
+                    print(f"{name}: VALU '{pop} {pdst}' writes {sorted(written & reads)} {ws} wait states before '{op}'")
+                    bad += 1
+                if pop.startswith("s_") and "m0" in written and ws < 1:
+                    print(f"{name}: SALU '{pop} {pdst}' writes m0 {ws} wait states before '{op}'")
+                    bad += 1
+                if pop == "s_nop":
+                    m = re.match(r"(0x[0-9a-f]+|\d+)", pdst)
+                    ws += (int(m.group(1), 0) if m else 0) + 1
+                else:
+                    ws += 1
+                if ws >= 5:
+                    break
+    return checked, bad
+
+
+def main():
+    lib = sys.argv[1] if len(sys.argv) > 1 else DEFAULT_LIB
+    checked, bad = check(parse(disassemble(lib)))
+    print(f"checked {checked} LDS-DMA loads; {bad} wait-state violation(s)")
+    return 1 if bad or checked == 0 else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
