@@ -660,6 +660,65 @@ def matcher_e2e(torch, device, stream, rank, sizes=(512, 1024, 2048), reps=10):
     return res
 
 
+def matcher_batched_pairs(torch, device, stream, rank, n=1024, pairs=(1, 4, 8, 16), reps=10, streams=2):
+    """BASELINE configs[4] on one GPU: P image pairs stacked in the batch dimension of ONE forward
+    (every projection and glue kernel runs once on all P pairs' rows; each layer's self and cross
+    attention is one grouped launch of P-batch calls), fp16, N0 = N1 = n; one captured forward
+    replayed back to back. Also `streams` such graphs of P pairs each replayed on that many streams
+    at once. pairs/s of the whole GPU."""
+    from lightglue_amd import matcher
+
+    model = matcher.LightGlueMatcher(n_layers=9).eval()
+    model.load_state_dict(matcher.seeded_state_dict(7, 9), strict=True)
+    model = model.to(device, torch.float16)
+    res = {}
+    for P in pairs:
+        graphs = []
+        for si in range(streams):
+            st = stream if si == 0 else torch.cuda.Stream(device)
+            ps = [matcher.synthetic_pair(80 + 31 * rank + 7 * si + i, n, n) for i in range(P)]
+            batch = tuple(torch.cat([p[j] for p in ps], 0).to(device, torch.float16) for j in range(4))
+            with torch.no_grad():
+                with torch.cuda.stream(st):
+                    for _ in range(2):
+                        model(*batch)  # warm: workspace + allocator outside the capture
+                st.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=st):
+                    out = model(*batch)
+            graphs.append((g, st, batch, out))
+        # one stream: events around `reps` back-to-back replays
+        g0, st0 = graphs[0][0], graphs[0][1]
+        g0.replay()
+        st0.synchronize()
+        s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s_.record(st0)
+        with torch.cuda.stream(st0):
+            for _ in range(reps):
+                g0.replay()
+        e_.record(st0)
+        st0.synchronize()
+        ms = s_.elapsed_time(e_) / reps
+        row = {"ms_per_forward": round(ms, 4), "pairs_per_s": round(P * 1e3 / ms, 1)}
+        # `streams` graphs of P pairs at once (host clock, best of reps rounds)
+        best = None
+        for rep in range(reps + 1):
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            for g, st, _, _ in graphs:
+                with torch.cuda.stream(st):
+                    g.replay()
+            torch.cuda.synchronize(device)
+            dt = time.perf_counter() - t0
+            if rep:
+                best = dt if best is None else min(best, dt)
+        row[f"pairs_per_s_{streams}_streams"] = round(streams * P / best, 1)
+        assert all(bool(torch.isfinite(o[2]).all()) for _, _, _, o in graphs)
+        res[str(P)] = row
+        del graphs
+    return res
+
+
 def matcher_pair_streams(torch, lightglue_amd, device, rank, n=1024, streams=(1, 2, 4, 8), reps=10):
     """BASELINE configs[4] on one GPU: a stream of independent image pairs through the end-to-end
     fp16 matcher, S pairs in flight (S streams, each replaying its own captured forward; the
@@ -1021,6 +1080,7 @@ def main():
         result["concurrent_streams"] = concurrent_streams(torch, lightglue_amd, device, nq, nkv, rank, flops)
         result["matcher_attention"] = matcher_attention(torch, device, stream, rank, separate=args.matcher_separate)
         result["matcher_e2e_fp16"] = matcher_e2e(torch, device, stream, rank)
+        result["matcher_batched_pairs_fp16"] = {"n": nq, "pairs": matcher_batched_pairs(torch, device, stream, rank, n=nq)}
         result["matcher_pair_streams_fp16"] = {"n": nq, "streams": matcher_pair_streams(torch, lightglue_amd, device,
                                                                                         rank, n=nq)}
         # whole-job pair rate (BASELINE configs[4]): each GPU streams its own pairs through the matcher
@@ -1028,11 +1088,15 @@ def main():
                             if str(nq) in result["matcher_e2e_fp16"] else None)
         stream_rates = gather(dist, max(v["pairs_per_s"] for v in
                                         result["matcher_pair_streams_fp16"]["streams"].values()))
+        batch_rates = gather(dist, max(max(v["pairs_per_s"], v.get("pairs_per_s_2_streams", 0.0)) for v in
+                                       result["matcher_batched_pairs_fp16"]["pairs"].values()))
         if all(p is not None for p in pair_rates):
             result["pairs_per_s_all_gpus"] = {"matcher_e2e_fp16": round(sum(pair_rates), 1), "n": nq,
                                               "per_rank": pair_rates,
                                               "pair_streams_best": round(sum(stream_rates), 1),
-                                              "pair_streams_per_rank": stream_rates}
+                                              "pair_streams_per_rank": stream_rates,
+                                              "batched_pairs_best": round(sum(batch_rates), 1),
+                                              "batched_pairs_per_rank": batch_rates}
 
     if args.sweep and rank == 0:
         sweep(torch, lib, device, stream, nq, nkv)

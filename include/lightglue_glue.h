@@ -7,6 +7,11 @@
  * Layouts are row-major and contiguous. dtype: MHA_HD64_DT_FLOAT (0) or MHA_HD64_DT_HALF (1)
  * for every tensor argument of a call (statistics and softmax math in fp32). All calls are
  * asynchronous on `stream` and return 0 or a nonzero status (message: mha_hd64_last_error()).
+ *
+ * Image pairs: the row-major side of the split/merge calls holds `pairs` image pairs stacked
+ * pair-major — pair p's n0 rows of image 0, then its n1 rows of image 1 — so "[n0+n1, ...]"
+ * below reads [pairs*(n0+n1), ...], and each per-image head-major tensor "[heads, ni, 64]" reads
+ * [pairs, heads, ni, 64] (the batch dimension of the attention calls). pairs = 1: one pair.
  */
 #ifndef LIGHTGLUE_GLUE_H_
 #define LIGHTGLUE_GLUE_H_
@@ -24,30 +29,30 @@ extern "C" {
  * output with channel (h*64 + d)*3 + j; cos/sin [n0+n1, 64] the positional encoding (pairs
  * repeated, lightglue.py:44-52). Writes q/k (rotated) and v of image i as [heads, ni, 64]. */
 int32_t lg_qkv_rotary_split(int32_t dtype, const void* qkv, const void* cos, const void* sin, int32_t heads,
-                            int32_t n0, int32_t n1, void* q0, void* k0, void* v0, void* q1, void* k1, void* v1,
-                            hipStream_t stream);
+                            int32_t n0, int32_t n1, int32_t pairs, void* q0, void* k0, void* v0, void* q1, void* k1,
+                            void* v1, hipStream_t stream);
 
 /* CrossBlock heads (lightglue.py:158-166): a, b [n0+n1, heads*64] -> a0, b0 [heads, n0, 64],
  * a1, b1 [heads, n1, 64]. */
 int32_t lg_split_heads2(int32_t dtype, const void* a, const void* b, int32_t heads, int32_t n0, int32_t n1,
-                        void* a0, void* a1, void* b0, void* b1, hipStream_t stream);
+                        int32_t pairs, void* a0, void* a1, void* b0, void* b1, hipStream_t stream);
 
 /* The same with row stride `ld` elements for a and b (column views of one wider projection, e.g.
  * the cross block's to_qk | to_v computed as one GEMM: a = qkv, b = qkv + heads*64, ld = 2*heads*64);
  * a and b 16-byte aligned. */
 int32_t lg_split_heads2_ld(int32_t dtype, const void* a, const void* b, int32_t ld, int32_t heads, int32_t n0,
-                           int32_t n1, void* a0, void* a1, void* b0, void* b1, hipStream_t stream);
+                           int32_t n1, int32_t pairs, void* a0, void* a1, void* b0, void* b1, hipStream_t stream);
 
 /* Attention outputs back to rows (lightglue.py:118-120, 163-170): x0 [heads, n0, 64],
  * x1 [heads, n1, 64] -> out [n0+n1, heads*64]. */
 int32_t lg_merge_heads(int32_t dtype, const void* x0, const void* x1, int32_t heads, int32_t n0, int32_t n1,
-                       void* out, hipStream_t stream);
+                       int32_t pairs, void* out, hipStream_t stream);
 
 /* The FFN input of both blocks (lightglue.py:104, 181: cat([x, message], -1)) with the message
  * projection folded into the FFN's first weight: out [n0+n1, 2*heads*64] = [x | merge(x0, x1)],
  * x [n0+n1, heads*64]. One pass instead of merge_heads + a concatenation copy. */
 int32_t lg_merge_heads_cat(int32_t dtype, const void* x, const void* x0, const void* x1, int32_t heads, int32_t n0,
-                           int32_t n1, void* out, hipStream_t stream);
+                           int32_t n1, int32_t pairs, void* out, hipStream_t stream);
 
 /* FFN middle (lightglue.py:101-106): y = GELU(LayerNorm(x) * gamma + beta), exact (erf) GELU,
  * x, y [rows, dim], dim a multiple of 64 and <= 1024. */
@@ -63,23 +68,24 @@ int32_t lg_linear(const void* a, const void* w, const void* bias, const void* re
 /* lg_linear_cat:        out [n0+n1, n] = [x | merge_heads(ctx0, ctx1)] · Wᵀ + bias with x [n0+n1, heads*64],
  *                       ctx_i [heads, ni, 64] (k = 2*heads*64; the FFN input of lightglue.py:104/181). */
 int32_t lg_linear_cat(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
-                      const void* w, const void* bias, int32_t n, void* out, hipStream_t stream);
+                      int32_t pairs, const void* w, const void* bias, int32_t n, void* out, hipStream_t stream);
 /* lg_linear_qkv_rotary: SelfBlock projection (lightglue.py:111-134) with W's rows and the bias in
  *                       [q|k|v][head][dim] order (row j*heads*64 + h*64 + d = Wqkv row (h*64+d)*3 + j):
  *                       rotary (cos/sin [n0+n1, 64]) on q and k, per-image head-major outputs. */
 int32_t lg_linear_qkv_rotary(const void* x, const void* w_perm, const void* b_perm, const void* cos, const void* sin,
-                             int32_t heads, int32_t n0, int32_t n1, int32_t k, void* q0, void* k0, void* v0, void* q1,
-                             void* k1, void* v1, hipStream_t stream);
+                             int32_t heads, int32_t n0, int32_t n1, int32_t pairs, int32_t k, void* q0, void* k0,
+                             void* v0, void* q1, void* k1, void* v1, hipStream_t stream);
 /* lg_linear_split2:     CrossBlock to_qk | to_v as one projection (W = [W_qk; W_v], lightglue.py:158-166):
  *                       per-image head-major a (= qk) and b (= v). */
 int32_t lg_linear_split2(const void* x, const void* w, const void* bias, int32_t heads, int32_t n0, int32_t n1,
-                         int32_t k, void* a0, void* a1, void* b0, void* b1, hipStream_t stream);
+                         int32_t pairs, int32_t k, void* a0, void* a1, void* b0, void* b1, hipStream_t stream);
 
 /* sigmoid_log_double_softmax (lightglue.py:197-205), fp32: scores[i][j] = 2 sim[i][j]
  * - logsumexp_j' sim[i][j'] - logsumexp_i' sim[i'][j] + logsigmoid(z0[i]) + logsigmoid(z1[j]).
- * sim, scores [m, n]; z0 [m], z1 [n]; workspace >= lg_log_double_softmax_workspace(m, n) bytes. */
-size_t lg_log_double_softmax_workspace(int32_t m, int32_t n);
-int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1, int32_t m, int32_t n,
+ * sim, scores [batch, m, n]; z0 [batch, m], z1 [batch, n] (batch image pairs, one launch);
+ * workspace >= lg_log_double_softmax_workspace(m, n, batch) bytes. */
+size_t lg_log_double_softmax_workspace(int32_t m, int32_t n, int32_t batch);
+int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1, int32_t m, int32_t n, int32_t batch,
                               float* scores, void* workspace, hipStream_t stream);
 
 #ifdef __cplusplus

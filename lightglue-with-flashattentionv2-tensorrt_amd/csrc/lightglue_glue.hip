@@ -19,14 +19,28 @@ template <typename T> __device__ __forceinline__ void st(T* p, float v) { *p = (
 
 constexpr int kD = 64;  // head dim
 
+// Row n of the stacked rows (`pairs` image pairs, pair-major: n0 rows of image 0, then n1 rows of
+// image 1) -> which image, and the offset of the row's head-h segment in that image's
+// [pairs, heads, ni, 64] tensor. pairs = 1 is the single-pair layout.
+struct ImgRow {
+    bool first;
+    size_t off;
+};
+__device__ __forceinline__ ImgRow img_row(int n, int n0, int n1, int heads, int h) {
+    const int ntot = n0 + n1;
+    const int p = n / ntot, l = n - p * ntot;
+    const bool first = l < n0;
+    const int row = first ? l : l - n0, nn = first ? n0 : n1;
+    return {first, (((size_t)p * heads + h) * nn + row) * kD};
+}
+
 // ---- q/k/v split + rotary (thread = one (row, head, rotary pair)) ----
 template <typename T>
 __global__ __launch_bounds__(256) void qkv_rotary_split_kernel(const T* __restrict__ qkv, const T* __restrict__ cosv,
                                                                const T* __restrict__ sinv, int heads, int n0, int n1,
-                                                               T* q0, T* k0, T* v0, T* q1, T* k1, T* v1) {
-    const int ntot = n0 + n1;
+                                                               int rows, T* q0, T* k0, T* v0, T* q1, T* k1, T* v1) {
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (long)ntot * heads * (kD / 2)) return;
+    if (idx >= (long)rows * heads * (kD / 2)) return;
     const int p = idx % (kD / 2);
     const int h = (idx / (kD / 2)) % heads;
     const int n = idx / ((long)(kD / 2) * heads);
@@ -35,9 +49,9 @@ __global__ __launch_bounds__(256) void qkv_rotary_split_kernel(const T* __restri
     const float q_a = ld(src + 0), k_a = ld(src + 1), v_a = ld(src + 2);
     const float q_b = ld(src + 3), k_b = ld(src + 4), v_b = ld(src + 5);
     const float c = ld(cosv + (size_t)n * kD + 2 * p), s = ld(sinv + (size_t)n * kD + 2 * p);
-    const bool first = n < n0;
-    const int row = first ? n : n - n0, nn = first ? n0 : n1;
-    const size_t o = ((size_t)h * nn + row) * kD + 2 * p;
+    const ImgRow ir = img_row(n, n0, n1, heads, h);
+    const bool first = ir.first;
+    const size_t o = ir.off + 2 * p;
     T* qd = first ? q0 : q1;
     T* kd = first ? k0 : k1;
     T* vd = first ? v0 : v1;
@@ -58,23 +72,22 @@ template <> struct V16<float> { typedef unsigned int type __attribute__((ext_vec
 // ---- [rows, heads*64] <-> per image [heads, ni, 64] (thread = one 16-B chunk) ----
 template <typename T, bool SPLIT>
 __global__ __launch_bounds__(256) void heads_kernel(const T* a, const T* b, T* a0, T* a1, T* b0, T* b1, int heads,
-                                                    int n0, int n1, int ld) {
+                                                    int n0, int n1, int rows, int ld) {
     typedef typename V16<T>::type vec;
     constexpr int E = V16<T>::n;
     constexpr int CH = kD / E;  // chunks per head row
-    const int ntot = n0 + n1;
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long per = (long)ntot * heads * CH;
+    const long per = (long)rows * heads * CH;
     if (idx >= (b ? 2 : 1) * per) return;
     const bool second = idx >= per;
     const long i = second ? idx - per : idx;
     const int c = i % CH;
     const int h = (i / CH) % heads;
     const int n = i / ((long)CH * heads);
-    const bool first = n < n0;
-    const int row = first ? n : n - n0, nn = first ? n0 : n1;
+    const ImgRow ir = img_row(n, n0, n1, heads, h);
+    const bool first = ir.first;
     const size_t rows_off = (size_t)n * ld + h * kD + c * E;  // row-major side: row stride ld
-    const size_t head_off = ((size_t)h * nn + row) * kD + c * E;
+    const size_t head_off = ir.off + c * E;
     if (SPLIT) {
         const T* src = second ? b : a;
         T* dst = second ? (first ? b0 : b1) : (first ? a0 : a1);
@@ -90,14 +103,13 @@ __global__ __launch_bounds__(256) void heads_kernel(const T* a, const T* b, T* a
 // head-major attention outputs.
 template <typename T>
 __global__ __launch_bounds__(256) void merge_cat_kernel(const T* x, const T* x0, const T* x1, T* out, int heads,
-                                                        int n0, int n1) {
+                                                        int n0, int n1, int rows) {
     typedef typename V16<T>::type vec;
     constexpr int E = V16<T>::n;
     constexpr int CH = kD / E;
-    const int ntot = n0 + n1;
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const int half = CH * heads;  // chunks per half row
-    if (idx >= (long)ntot * 2 * half) return;
+    if (idx >= (long)rows * 2 * half) return;
     const int cc = idx % (2 * half);
     const int n = idx / (2 * half);
     vec v;
@@ -105,9 +117,8 @@ __global__ __launch_bounds__(256) void merge_cat_kernel(const T* x, const T* x0,
         v = *reinterpret_cast<const vec*>(x + (size_t)n * heads * kD + cc * E);
     } else {
         const int c2 = cc - half, h = c2 / CH, c = c2 % CH;
-        const bool first = n < n0;
-        const int row = first ? n : n - n0, nn = first ? n0 : n1;
-        v = *reinterpret_cast<const vec*>((first ? x0 : x1) + ((size_t)h * nn + row) * kD + c * E);
+        const ImgRow ir = img_row(n, n0, n1, heads, h);
+        v = *reinterpret_cast<const vec*>((ir.first ? x0 : x1) + ir.off + c * E);
     }
     *reinterpret_cast<vec*>(out + (size_t)n * 2 * heads * kD + cc * E) = v;
 }
@@ -212,7 +223,11 @@ __device__ __forceinline__ void lse_merge(float& mx, float& s, float m2, float s
 }
 
 __global__ __launch_bounds__(256) void lse_kernel(const float* __restrict__ sim, int m, int n, int rb,
-                                                  float* lse_row, float2* col_part) {
+                                                  float* lse_row, float2* col_part, size_t ws_stride) {
+    // blockIdx.y: the pair of a batched launch (its sim slice and workspace slice)
+    sim += (size_t)blockIdx.y * m * n;
+    lse_row = reinterpret_cast<float*>(reinterpret_cast<char*>(lse_row) + blockIdx.y * ws_stride);
+    col_part = reinterpret_cast<float2*>(reinterpret_cast<char*>(col_part) + blockIdx.y * ws_stride);
     if ((int)blockIdx.x < rb) {
         const int lane = threadIdx.x & 63;
         const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -260,7 +275,13 @@ __device__ __forceinline__ float log_sigmoid(float z) { return fminf(z, 0.f) - l
 __global__ __launch_bounds__(256) void dual_combine_kernel(const float* __restrict__ sim, const float* z0,
                                                            const float* z1, const float* lse_row,
                                                            const float2* col_part, int chunks, int m, int n,
-                                                           float* out) {
+                                                           float* out, size_t ws_stride) {
+    sim += (size_t)blockIdx.y * m * n;
+    out += (size_t)blockIdx.y * m * n;
+    z0 += (size_t)blockIdx.y * m;
+    z1 += (size_t)blockIdx.y * n;
+    lse_row = reinterpret_cast<const float*>(reinterpret_cast<const char*>(lse_row) + blockIdx.y * ws_stride);
+    col_part = reinterpret_cast<const float2*>(reinterpret_cast<const char*>(col_part) + blockIdx.y * ws_stride);
     const int cblocks = (n + 255) / 256;
     const int j = (blockIdx.x % cblocks) * 256 + threadIdx.x;
     const int i0 = (blockIdx.x / cblocks) * kCombRows;
@@ -292,78 +313,81 @@ bool bad_dtype(int32_t dt) { return dt != MHA_HD64_DT_HALF && dt != MHA_HD64_DT_
 extern "C" {
 
 int32_t lg_qkv_rotary_split(int32_t dtype, const void* qkv, const void* cosv, const void* sinv, int32_t heads,
-                            int32_t n0, int32_t n1, void* q0, void* k0, void* v0, void* q1, void* k1, void* v1,
-                            hipStream_t stream) {
-    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || !qkv || !cosv || !sinv)
+                            int32_t n0, int32_t n1, int32_t pairs, void* q0, void* k0, void* v0, void* q1, void* k1,
+                            void* v1, hipStream_t stream) {
+    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || pairs < 0 || !qkv || !cosv || !sinv)
         return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_qkv_rotary_split", "bad arguments");
-    const long threads = (long)(n0 + n1) * heads * (kD / 2);
+    const int rows = pairs * (n0 + n1);
+    const long threads = (long)rows * heads * (kD / 2);
     if (threads == 0) return MHA_HD64_STATUS_SUCCESS;
     if (dtype == MHA_HD64_DT_HALF)
         hipLaunchKernelGGL(qkv_rotary_split_kernel<f16>, dim3(blocks_for(threads)), dim3(256), 0, stream,
-                           (const f16*)qkv, (const f16*)cosv, (const f16*)sinv, heads, n0, n1, (f16*)q0, (f16*)k0,
-                           (f16*)v0, (f16*)q1, (f16*)k1, (f16*)v1);
+                           (const f16*)qkv, (const f16*)cosv, (const f16*)sinv, heads, n0, n1, rows, (f16*)q0,
+                           (f16*)k0, (f16*)v0, (f16*)q1, (f16*)k1, (f16*)v1);
     else
         hipLaunchKernelGGL(qkv_rotary_split_kernel<float>, dim3(blocks_for(threads)), dim3(256), 0, stream,
-                           (const float*)qkv, (const float*)cosv, (const float*)sinv, heads, n0, n1, (float*)q0,
+                           (const float*)qkv, (const float*)cosv, (const float*)sinv, heads, n0, n1, rows, (float*)q0,
                            (float*)k0, (float*)v0, (float*)q1, (float*)k1, (float*)v1);
     return launched("lg_qkv_rotary_split");
 }
 
 int32_t lg_split_heads2(int32_t dtype, const void* a, const void* b, int32_t heads, int32_t n0, int32_t n1,
-                        void* a0, void* a1, void* b0, void* b1, hipStream_t stream) {
-    return lg_split_heads2_ld(dtype, a, b, heads * kD, heads, n0, n1, a0, a1, b0, b1, stream);
+                        int32_t pairs, void* a0, void* a1, void* b0, void* b1, hipStream_t stream) {
+    return lg_split_heads2_ld(dtype, a, b, heads * kD, heads, n0, n1, pairs, a0, a1, b0, b1, stream);
 }
 
 int32_t lg_split_heads2_ld(int32_t dtype, const void* a, const void* b, int32_t ld, int32_t heads, int32_t n0,
-                           int32_t n1, void* a0, void* a1, void* b0, void* b1, hipStream_t stream) {
+                           int32_t n1, int32_t pairs, void* a0, void* a1, void* b0, void* b1, hipStream_t stream) {
     const int E = dtype == MHA_HD64_DT_HALF ? 8 : 4;
-    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || !a || ld < heads * kD || ld % E != 0 ||
+    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || pairs < 0 || !a || ld < heads * kD || ld % E != 0 ||
         (reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) % 16 != 0)
         return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_split_heads2", "bad arguments");
-    
-    const long threads = (b ? 2 : 1) * (long)(n0 + n1) * heads * (kD / E);
+    const int rows = pairs * (n0 + n1);
+    const long threads = (b ? 2 : 1) * (long)rows * heads * (kD / E);
     if (threads == 0) return MHA_HD64_STATUS_SUCCESS;
     if (dtype == MHA_HD64_DT_HALF)
         hipLaunchKernelGGL((heads_kernel<f16, true>), dim3(blocks_for(threads)), dim3(256), 0, stream, (const f16*)a,
-                           (const f16*)b, (f16*)a0, (f16*)a1, (f16*)b0, (f16*)b1, heads, n0, n1, ld);
+                           (const f16*)b, (f16*)a0, (f16*)a1, (f16*)b0, (f16*)b1, heads, n0, n1, rows, ld);
     else
         hipLaunchKernelGGL((heads_kernel<float, true>), dim3(blocks_for(threads)), dim3(256), 0, stream,
                            (const float*)a, (const float*)b, (float*)a0, (float*)a1, (float*)b0, (float*)b1, heads,
-                           n0, n1, ld);
+                           n0, n1, rows, ld);
     return launched("lg_split_heads2");
 }
 
 int32_t lg_merge_heads(int32_t dtype, const void* x0, const void* x1, int32_t heads, int32_t n0, int32_t n1,
-                       void* out, hipStream_t stream) {
-    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || !out)
+                       int32_t pairs, void* out, hipStream_t stream) {
+    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || pairs < 0 || !out)
         return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_merge_heads", "bad arguments");
     const int E = dtype == MHA_HD64_DT_HALF ? 8 : 4;
-    const long threads = (long)(n0 + n1) * heads * (kD / E);
+    const int rows = pairs * (n0 + n1);
+    const long threads = (long)rows * heads * (kD / E);
     if (threads == 0) return MHA_HD64_STATUS_SUCCESS;
     if (dtype == MHA_HD64_DT_HALF)
         hipLaunchKernelGGL((heads_kernel<f16, false>), dim3(blocks_for(threads)), dim3(256), 0, stream,
-                           (const f16*)x0, (const f16*)x1, (f16*)out, nullptr, nullptr, nullptr, heads, n0, n1,
+                           (const f16*)x0, (const f16*)x1, (f16*)out, nullptr, nullptr, nullptr, heads, n0, n1, rows,
                            heads * kD);
     else
         hipLaunchKernelGGL((heads_kernel<float, false>), dim3(blocks_for(threads)), dim3(256), 0, stream,
                            (const float*)x0, (const float*)x1, (float*)out, nullptr, nullptr, nullptr, heads, n0,
-                           n1, heads * kD);
+                           n1, rows, heads * kD);
     return launched("lg_merge_heads");
 }
 
 int32_t lg_merge_heads_cat(int32_t dtype, const void* x, const void* x0, const void* x1, int32_t heads, int32_t n0,
-                           int32_t n1, void* out, hipStream_t stream) {
-    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || !x || !out)
+                           int32_t n1, int32_t pairs, void* out, hipStream_t stream) {
+    if (bad_dtype(dtype) || heads <= 0 || n0 < 0 || n1 < 0 || pairs < 0 || !x || !out)
         return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_merge_heads_cat", "bad arguments");
     const int E = dtype == MHA_HD64_DT_HALF ? 8 : 4;
-    const long threads = (long)(n0 + n1) * 2 * heads * (kD / E);
+    const int rows = pairs * (n0 + n1);
+    const long threads = (long)rows * 2 * heads * (kD / E);
     if (threads == 0) return MHA_HD64_STATUS_SUCCESS;
     if (dtype == MHA_HD64_DT_HALF)
         hipLaunchKernelGGL((merge_cat_kernel<f16>), dim3(blocks_for(threads)), dim3(256), 0, stream, (const f16*)x,
-                           (const f16*)x0, (const f16*)x1, (f16*)out, heads, n0, n1);
+                           (const f16*)x0, (const f16*)x1, (f16*)out, heads, n0, n1, rows);
     else
         hipLaunchKernelGGL((merge_cat_kernel<float>), dim3(blocks_for(threads)), dim3(256), 0, stream,
-                           (const float*)x, (const float*)x0, (const float*)x1, (float*)out, heads, n0, n1);
+                           (const float*)x, (const float*)x0, (const float*)x1, (float*)out, heads, n0, n1, rows);
     return launched("lg_merge_heads_cat");
 }
 
@@ -399,27 +423,35 @@ int32_t lg_layernorm_gelu(int32_t dtype, const void* x, const void* gamma, const
     return launched("lg_layernorm_gelu");
 }
 
-size_t lg_log_double_softmax_workspace(int32_t m, int32_t n) {
-    if (m <= 0 || n <= 0) return 0;
+namespace {
+size_t dual_ws_stride(int32_t m, int32_t n) {  // one pair's workspace slice (256-B aligned)
     const size_t chunks = (size_t)(m + kColChunk - 1) / kColChunk;
-    return ((size_t)m * sizeof(float) + 15) / 16 * 16 + chunks * (size_t)n * sizeof(float2);
+    const size_t b = ((size_t)m * sizeof(float) + 15) / 16 * 16 + chunks * (size_t)n * sizeof(float2);
+    return (b + 255) / 256 * 256;
+}
+}  // namespace
+
+size_t lg_log_double_softmax_workspace(int32_t m, int32_t n, int32_t batch) {
+    if (m <= 0 || n <= 0 || batch <= 0) return 0;
+    return dual_ws_stride(m, n) * (size_t)batch;
 }
 
-int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1, int32_t m, int32_t n, float* scores,
-                              void* workspace, hipStream_t stream) {
-    if (m < 0 || n < 0 || ((m > 0 && n > 0) && (!sim || !z0 || !z1 || !scores || !workspace)))
+int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1, int32_t m, int32_t n,
+                              int32_t batch, float* scores, void* workspace, hipStream_t stream) {
+    if (m < 0 || n < 0 || batch < 0 || ((m > 0 && n > 0 && batch > 0) && (!sim || !z0 || !z1 || !scores || !workspace)))
         return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_log_double_softmax", "bad arguments");
-    if (m == 0 || n == 0) return MHA_HD64_STATUS_SUCCESS;
+    if (m == 0 || n == 0 || batch == 0) return MHA_HD64_STATUS_SUCCESS;
+    const size_t ws_stride = dual_ws_stride(m, n);
     float* lse_row = reinterpret_cast<float*>(workspace);
     float2* col_part = reinterpret_cast<float2*>(reinterpret_cast<char*>(workspace) +
                                                  ((size_t)m * sizeof(float) + 15) / 16 * 16);
     const int rb = (m + 3) / 4;
     const int chunks = (m + kColChunk - 1) / kColChunk;
     const int cblocks = (n + 63) / 64;
-    hipLaunchKernelGGL(lse_kernel, dim3(rb + chunks * cblocks), dim3(256), 0, stream, sim, m, n, rb, lse_row,
-                       col_part);
-    hipLaunchKernelGGL(dual_combine_kernel, dim3(((m + kCombRows - 1) / kCombRows) * ((n + 255) / 256)), dim3(256), 0,
-                       stream, sim, z0, z1, lse_row, col_part, chunks, m, n, scores);
+    hipLaunchKernelGGL(lse_kernel, dim3(rb + chunks * cblocks, batch), dim3(256), 0, stream, sim, m, n, rb, lse_row,
+                       col_part, ws_stride);
+    hipLaunchKernelGGL(dual_combine_kernel, dim3(((m + kCombRows - 1) / kCombRows) * ((n + 255) / 256), batch),
+                       dim3(256), 0, stream, sim, z0, z1, lse_row, col_part, chunks, m, n, scores, ws_stride);
     return launched("lg_log_double_softmax");
 }
 

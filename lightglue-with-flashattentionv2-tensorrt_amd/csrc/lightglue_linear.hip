@@ -55,9 +55,23 @@ struct LinArgs {
     const f16* sinv;
     f16* out[6];       // EPI_BIAS: out[0] [m, n]; QKV: q0 k0 v0 q1 k1 v1; SPLIT2: a0 a1 b0 b1
     int m, n, k;
-    int heads, n0;     // per-image split (n0 rows of image 0; m - n0 of image 1)
+    int heads, n0, n1; // per-image split: m = pairs x (n0 + n1) rows, pair-major (n0 of image 0, n1 of image 1)
     int mtiles, total;
 };
+
+// Row `row` of the stacked rows -> its image and the offset of its head-h segment in that image's
+// [pairs, heads, ni, 64] tensor
+struct LinRow {
+    bool first;
+    size_t off;
+};
+__device__ __forceinline__ LinRow lin_row(const LinArgs& p, int row, int h) {
+    const int ntot = p.n0 + p.n1;
+    const int pr = row / ntot, l = row - pr * ntot;
+    const bool first = l < p.n0;
+    const int r = first ? l : l - p.n0, nn = first ? p.n0 : p.n1;
+    return {first, (((size_t)pr * p.heads + h) * nn + r) * kD};
+}
 
 // global source of A row `row`, 16-B unit `gc` (8 k values)
 template <bool GATHER>
@@ -68,9 +82,8 @@ __device__ __forceinline__ const f16* a_src(const LinArgs& p, int row, int gc) {
         const int half = p.k / 2, col = gc * 8;
         if (col < half) return p.a + (size_t)row * half + col;  // x
         const int c2 = col - half, h = c2 / kD, d = c2 % kD;
-        const bool first = row < p.n0;
-        const int r = first ? row : row - p.n0, nn = first ? p.n0 : p.m - p.n0;
-        return (first ? p.ctx0 : p.ctx1) + ((size_t)h * nn + r) * kD + d;
+        const LinRow lr = lin_row(p, row, h);
+        return (lr.first ? p.ctx0 : p.ctx1) + lr.off + d;
     }
 }
 
@@ -174,8 +187,8 @@ __global__ __launch_bounds__(256) void linear_kernel(LinArgs p) {
         } else {
             const int hd = p.heads * kD;
             const int part = n / hd, h = (n % hd) / kD, d = n % kD;
-            const bool first = m < p.n0;
-            const int row = first ? m : m - p.n0, nn = first ? p.n0 : p.m - p.n0;
+            const LinRow lr = lin_row(p, m, h);
+            const bool first = lr.first;
             if constexpr (EPI == EPI_QKV_ROTARY) {
                 if (part < 2) {  // q, k: (x0, x1) -> (x0 c - x1 s, x1 c + x0 s), pairs (d, d+1)
                     const f16x4 cc = aux0[g], ss = aux1[g];
@@ -188,7 +201,7 @@ __global__ __launch_bounds__(256) void linear_kernel(LinArgs p) {
                 }
             }
             f16* dst = p.out[(first ? 0 : (EPI == EPI_QKV_ROTARY ? 3 : 1)) + (EPI == EPI_QKV_ROTARY ? part : 2 * part)];
-            *reinterpret_cast<f16x4*>(dst + ((size_t)h * nn + row) * kD + d) =
+            *reinterpret_cast<f16x4*>(dst + lr.off + d) =
                 f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
         }
     }
@@ -226,29 +239,29 @@ int32_t lg_linear(const void* a, const void* w, const void* bias, const void* re
     LinArgs p{};
     p.a = (const f16*)a, p.w = (const f16*)w, p.bias = (const f16*)bias, p.res = (const f16*)res;
     p.out[0] = (f16*)out;
-    p.m = m, p.n = n, p.k = k, p.n0 = m;
+    p.m = m, p.n = n, p.k = k, p.n0 = m, p.n1 = 0;
     return launch<EPI_BIAS, false>(p, stream, "lg_linear");
 }
 
 int32_t lg_linear_cat(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
-                      const void* w, const void* bias, int32_t n, void* out, hipStream_t stream) {
-    const int k = 2 * heads * kD, m = n0 + n1;
-    if (heads <= 0 || n0 < 0 || n1 < 0 || !shape_ok(m, n, k) || !x || !w || !bias || !out || !aligned16(x) ||
+                      int32_t pairs, const void* w, const void* bias, int32_t n, void* out, hipStream_t stream) {
+    const int k = 2 * heads * kD, m = pairs * (n0 + n1);
+    if (heads <= 0 || n0 < 0 || n1 < 0 || pairs < 0 || !shape_ok(m, n, k) || !x || !w || !bias || !out || !aligned16(x) ||
         (n0 && !aligned16(ctx0)) || (n1 && !aligned16(ctx1)) || !aligned16(w) || !aligned8(bias) || !aligned8(out))
         return bad("lg_linear_cat");
     if (m == 0) return MHA_HD64_STATUS_SUCCESS;
     LinArgs p{};
     p.a = (const f16*)x, p.ctx0 = (const f16*)ctx0, p.ctx1 = (const f16*)ctx1, p.w = (const f16*)w;
     p.bias = (const f16*)bias, p.out[0] = (f16*)out;
-    p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0;
+    p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
     return launch<EPI_BIAS, true>(p, stream, "lg_linear_cat");
 }
 
 int32_t lg_linear_qkv_rotary(const void* x, const void* w_perm, const void* b_perm, const void* cosv,
-                             const void* sinv, int32_t heads, int32_t n0, int32_t n1, int32_t k, void* q0, void* k0,
-                             void* v0, void* q1, void* k1, void* v1, hipStream_t stream) {
-    const int m = n0 + n1, n = 3 * heads * kD;
-    if (heads <= 0 || n0 < 0 || n1 < 0 || !shape_ok(m, n, k) || !x || !w_perm || !b_perm || !cosv || !sinv ||
+                             const void* sinv, int32_t heads, int32_t n0, int32_t n1, int32_t pairs, int32_t k,
+                             void* q0, void* k0, void* v0, void* q1, void* k1, void* v1, hipStream_t stream) {
+    const int m = pairs * (n0 + n1), n = 3 * heads * kD;
+    if (heads <= 0 || n0 < 0 || n1 < 0 || pairs < 0 || !shape_ok(m, n, k) || !x || !w_perm || !b_perm || !cosv || !sinv ||
         !aligned16(x) || !aligned16(w_perm) || !aligned8(b_perm) || !aligned8(cosv) || !aligned8(sinv))
         return bad("lg_linear_qkv_rotary");
     if (m == 0) return MHA_HD64_STATUS_SUCCESS;
@@ -257,14 +270,14 @@ int32_t lg_linear_qkv_rotary(const void* x, const void* w_perm, const void* b_pe
     p.cosv = (const f16*)cosv, p.sinv = (const f16*)sinv;
     f16* outs[6] = {(f16*)q0, (f16*)k0, (f16*)v0, (f16*)q1, (f16*)k1, (f16*)v1};
     for (int i = 0; i < 6; ++i) p.out[i] = outs[i];
-    p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0;
+    p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
     return launch<EPI_QKV_ROTARY, false>(p, stream, "lg_linear_qkv_rotary");
 }
 
 int32_t lg_linear_split2(const void* x, const void* w, const void* bias, int32_t heads, int32_t n0, int32_t n1,
-                         int32_t k, void* a0, void* a1, void* b0, void* b1, hipStream_t stream) {
-    const int m = n0 + n1, n = 2 * heads * kD;
-    if (heads <= 0 || n0 < 0 || n1 < 0 || !shape_ok(m, n, k) || !x || !w || !bias || !aligned16(x) ||
+                         int32_t pairs, int32_t k, void* a0, void* a1, void* b0, void* b1, hipStream_t stream) {
+    const int m = pairs * (n0 + n1), n = 2 * heads * kD;
+    if (heads <= 0 || n0 < 0 || n1 < 0 || pairs < 0 || !shape_ok(m, n, k) || !x || !w || !bias || !aligned16(x) ||
         !aligned16(w) || !aligned8(bias))
         return bad("lg_linear_split2");
     if (m == 0) return MHA_HD64_STATUS_SUCCESS;
@@ -272,7 +285,7 @@ int32_t lg_linear_split2(const void* x, const void* w, const void* bias, int32_t
     p.a = (const f16*)x, p.w = (const f16*)w, p.bias = (const f16*)bias;
     f16* outs[4] = {(f16*)a0, (f16*)a1, (f16*)b0, (f16*)b1};
     for (int i = 0; i < 4; ++i) p.out[i] = outs[i];
-    p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0;
+    p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
     return launch<EPI_SPLIT2, false>(p, stream, "lg_linear_split2");
 }
 

@@ -348,7 +348,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
     for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) pB[jj][ss] = f16x8{};
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 2) * kPiece) : "memory");
+    // Q and tile 0 first: tile 0's QKᵀ below runs while tile 1 lands
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 1) * kPiece) : "memory");
     __builtin_amdgcn_s_barrier();
 #ifdef MHA_STREAM_STAMPS
     SCLK(ck_pro);
@@ -446,7 +447,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         constexpr bool FIRST = KIND == 0;
         constexpr bool PV = true;  // a P·V of global tile g − 1 in phase B
         constexpr bool LAST = KIND == 3;
-        constexpr bool MASK = KIND == 0 || KIND == 2 || KIND == 3 || KIND == 5;  // tile t + 1 may hold keys past nkv
+        constexpr bool MASK = KIND != 1 && KIND != 4;  // tile t + 1 may hold keys past nkv
         constexpr bool BAR = NW == 4 || KIND == 1 || KIND == 2 || KIND == 3;  // (NW 8: odd t)
         const unsigned g = gb + (unsigned)t;
 #ifdef MHA_STREAM_PRIO_BAL
@@ -459,11 +460,17 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         const unsigned vbase = ((g - 1u) & kSM) * (unsigned)kSSlot;  // V of tile t − 1
         // FIRST: tile 0's scores came from a C = 0 chain (the previous item's last step, or the
         // kernel prologue); its exact row max becomes the item's running max
+        // (m = 0 while every query's tile-0 max lies within ±kRescaleThr of 0: P <= 2^8 and the
+        // largest P of a row >= 2^-8, no subtraction; else, rare, the exact max)
         if constexpr (FIRST) {
-            const float d = (c.mx < kEmptyMax) ? 0.f : c.mx;  // (never empty: nkv >= 1)
-            cm = splat16(-d);
-            c.s0 -= d;
-            c.s1 -= d;
+            cm = f32x16{};
+            if (__builtin_amdgcn_ballot_w64(fabsf(c.mx) > kRescaleThr) != 0) {
+                asm volatile("" ::: "memory");  // (a real branch)
+                const float d = (c.mx < kEmptyMax) ? 0.f : c.mx;  // (never empty: nkv >= 1)
+                cm = splat16(-d);
+                c.s0 -= d;
+                c.s1 -= d;
+            }
         }
         // online-softmax decision for tile t (rare): the max moves now for tiles t, t + 1, ...;
         // O and l follow after tile t − 1's P·V (at the old max) is in
@@ -527,7 +534,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
             if (gi >= 14 && gi < 18) maxk(gi - 14);
         };
 
-        constexpr int SB = KIND == 0 ? 2 : (KIND == 1 || KIND == 4) ? 6 : (KIND == 2 || KIND == 5) ? 10 : 16;  // (stamps)
+        constexpr int SB = KIND == 0 ? 2 : (KIND == 1 || KIND == 4) ? 6 : KIND == 3 ? 16 : 10;  // (stamps)
         int gi = 0;
         // phase A: QKᵀ(t + 1), each gap an exponential pair (+ LDS reads, DMA pieces, packs). In
         // the LAST step, tile t + 1 is the next item's tile 0 (global tile g + 1, landed two
@@ -657,6 +664,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         if (cur.nkv < kTileKV) mask_tile(sA, cur.nkv);
         sA.mx = xhalf_max(tree_max(sA.s0, sA.s1));
     }
+    // tile 1 (read by the first FIRST step) landed everywhere
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 2) * kPiece) : "memory");
+    __builtin_amdgcn_s_barrier();
 #ifdef MHA_STREAM_STAMPS
     SCLK(ck_t0);
     ck_sum[0] += ck_t0 - ck_pro;
@@ -694,9 +704,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
             step(K5{}, t + 1, sA, sB, pB, pA);
         }
         // the last step: beside tile nt − 2's P·V, the next item's tile 0 (its Q first: the
-        // current item's fragments are no longer needed); tile nt − 1's P·V and this item's
+        // current item's fragments are no longer needed; NW 8 two-tile items: once this wave's DMA
+        // of it, issued before the FIRST step, has landed); tile nt − 1's P·V and this item's
         // epilogue follow in the next item's FIRST step
         SEG(14);
+        if (NW == 8 && nt == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned qbad_next = read_q();
         SEG(15);
         step(K3{}, t, sB, sA, pA, pB);

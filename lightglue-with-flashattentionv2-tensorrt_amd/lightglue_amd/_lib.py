@@ -125,18 +125,18 @@ SIGNATURES = {
 # include/lightglue_glue.h (matcher kernels around the op)
 _F = ctypes.POINTER(ctypes.c_float)
 SIGNATURES.update({
-    "lg_qkv_rotary_split": ([_I, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P], _I),
-    "lg_split_heads2": ([_I, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P], _I),
-    "lg_merge_heads": ([_I, _P, _P, _I, _I, _I, _P, _P], _I),
-    "lg_split_heads2_ld": ([_I, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P], _I),
-    "lg_merge_heads_cat": ([_I, _P, _P, _P, _I, _I, _I, _P, _P], _I),
+    "lg_qkv_rotary_split": ([_I, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P], _I),
+    "lg_split_heads2": ([_I, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P], _I),
+    "lg_merge_heads": ([_I, _P, _P, _I, _I, _I, _I, _P, _P], _I),
+    "lg_split_heads2_ld": ([_I, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P], _I),
+    "lg_merge_heads_cat": ([_I, _P, _P, _P, _I, _I, _I, _I, _P, _P], _I),
     "lg_linear": ([_P, _P, _P, _P, _I, _I, _I, _P, _P], _I),
-    "lg_linear_cat": ([_P, _P, _P, _I, _I, _I, _P, _P, _I, _P, _P], _I),
-    "lg_linear_qkv_rotary": ([_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P], _I),
-    "lg_linear_split2": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P], _I),
+    "lg_linear_cat": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P, _P], _I),
+    "lg_linear_qkv_rotary": ([_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P], _I),
+    "lg_linear_split2": ([_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P], _I),
     "lg_layernorm_gelu": ([_I, _P, _P, _P, _I, _I, ctypes.c_float, _P, _P], _I),
-    "lg_log_double_softmax_workspace": ([_I, _I], _S),
-    "lg_log_double_softmax": ([_P, _P, _P, _I, _I, _P, _P, _P], _I),
+    "lg_log_double_softmax_workspace": ([_I, _I, _I], _S),
+    "lg_log_double_softmax": ([_P, _P, _P, _I, _I, _I, _P, _P, _P], _I),
     # kernel-form switches (include/mha_hd64.h "kernel-form switches")
     "mha_hd64_set_fused_combine": ([_I], None),
     "mha_hd64_set_f32_inkernel": ([_I], None),

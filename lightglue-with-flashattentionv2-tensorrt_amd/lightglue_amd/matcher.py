@@ -42,8 +42,15 @@ AttnFn = Callable[[Sequence[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]]], L
 _DT = {torch.float16: _lib.DT_HALF, torch.float32: _lib.DT_FLOAT}
 
 
+def _sp(splits):
+    """(n0, n1[, pairs]) -> (n0, n1, pairs): rows are `pairs` image pairs stacked pair-major."""
+    return (splits[0], splits[1], splits[2] if len(splits) > 2 else 1)
+
+
 class _Hip:
-    """Thin wrappers of the gfx950 glue kernels (current stream, fail loudly on error)."""
+    """Thin wrappers of the gfx950 glue kernels (current stream, fail loudly on error). Row-major
+    tensors hold P image pairs stacked pair-major ([1, P*(n0+n1), C]); per-image head-major
+    tensors are [P, heads, ni, 64] (include/lightglue_glue.h)."""
 
     @staticmethod
     def _stream(t):
@@ -51,45 +58,45 @@ class _Hip:
 
     @staticmethod
     def qkv_rotary_split(qkv, cos, sin, heads, splits):
-        n0, n1 = splits
-        mk = lambda n: torch.empty((1, heads, n, 64), dtype=qkv.dtype, device=qkv.device)  # noqa: E731
+        n0, n1, pr = _sp(splits)
+        mk = lambda n: torch.empty((pr, heads, n, 64), dtype=qkv.dtype, device=qkv.device)  # noqa: E731
         out = [tuple(mk(n) for _ in range(3)) for n in (n0, n1)]
         st = _lib.load().lg_qkv_rotary_split(_DT[qkv.dtype], qkv.data_ptr(), cos.data_ptr(), sin.data_ptr(), heads,
-                                             n0, n1, *(t.data_ptr() for t in out[0]),
+                                             n0, n1, pr, *(t.data_ptr() for t in out[0]),
                                              *(t.data_ptr() for t in out[1]), _Hip._stream(qkv))
         _check(st, "lg_qkv_rotary_split")
         return out
 
     @staticmethod
     def split_heads2(a, b, heads, splits):
-        n0, n1 = splits
-        mk = lambda n: torch.empty((1, heads, n, 64), dtype=a.dtype, device=a.device)  # noqa: E731
+        n0, n1, pr = _sp(splits)
+        mk = lambda n: torch.empty((pr, heads, n, 64), dtype=a.dtype, device=a.device)  # noqa: E731
         a0, a1, b0, b1 = mk(n0), mk(n1), mk(n0), mk(n1)
-        st = _lib.load().lg_split_heads2(_DT[a.dtype], a.data_ptr(), b.data_ptr(), heads, n0, n1, a0.data_ptr(),
+        st = _lib.load().lg_split_heads2(_DT[a.dtype], a.data_ptr(), b.data_ptr(), heads, n0, n1, pr, a0.data_ptr(),
                                          a1.data_ptr(), b0.data_ptr(), b1.data_ptr(), _Hip._stream(a))
         _check(st, "lg_split_heads2")
         return (a0, a1), (b0, b1)
 
     @staticmethod
     def split_heads2_ld(ab, heads, splits):
-        """ab [1, N0+N1, 2*heads*64] = [a | b] (one GEMM's output) -> per image (a_i, b_i) heads."""
-        n0, n1 = splits
-        mk = lambda n: torch.empty((1, heads, n, 64), dtype=ab.dtype, device=ab.device)  # noqa: E731
+        """ab [1, P*(N0+N1), 2*heads*64] = [a | b] (one GEMM's output) -> per image (a_i, b_i) heads."""
+        n0, n1, pr = _sp(splits)
+        mk = lambda n: torch.empty((pr, heads, n, 64), dtype=ab.dtype, device=ab.device)  # noqa: E731
         a0, a1, b0, b1 = mk(n0), mk(n1), mk(n0), mk(n1)
         half = heads * 64
         st = _lib.load().lg_split_heads2_ld(_DT[ab.dtype], ab.data_ptr(), ab.data_ptr() + half * ab.element_size(),
-                                            2 * half, heads, n0, n1, a0.data_ptr(), a1.data_ptr(), b0.data_ptr(),
+                                            2 * half, heads, n0, n1, pr, a0.data_ptr(), a1.data_ptr(), b0.data_ptr(),
                                             b1.data_ptr(), _Hip._stream(ab))
         _check(st, "lg_split_heads2_ld")
         return (a0, a1), (b0, b1)
 
     @staticmethod
     def merge_heads_cat(x, x0, x1):
-        """[x | merge_heads(x0, x1)] -> [1, N0+N1, 2*heads*64] (the FFN input)."""
-        heads, n0, n1 = x0.shape[1], x0.shape[2], x1.shape[2]
-        out = torch.empty((1, n0 + n1, 2 * heads * 64), dtype=x.dtype, device=x.device)
+        """[x | merge_heads(x0, x1)] -> [1, P*(N0+N1), 2*heads*64] (the FFN input)."""
+        pr, heads, n0, n1 = x0.shape[0], x0.shape[1], x0.shape[2], x1.shape[2]
+        out = torch.empty((1, pr * (n0 + n1), 2 * heads * 64), dtype=x.dtype, device=x.device)
         st = _lib.load().lg_merge_heads_cat(_DT[x.dtype], x.data_ptr(), x0.data_ptr(), x1.data_ptr(), heads, n0, n1,
-                                            out.data_ptr(), _Hip._stream(x))
+                                            pr, out.data_ptr(), _Hip._stream(x))
         _check(st, "lg_merge_heads_cat")
         return out
 
@@ -107,20 +114,20 @@ class _Hip:
     @staticmethod
     def linear_cat(x, c0, c1, w, b):
         """[x | merge_heads(c0, c1)]·wᵀ + b."""
-        heads, n0, n1 = c0.shape[1], c0.shape[2], c1.shape[2]
-        out = torch.empty((1, n0 + n1, w.shape[0]), dtype=x.dtype, device=x.device)
-        st = _lib.load().lg_linear_cat(x.data_ptr(), c0.data_ptr(), c1.data_ptr(), heads, n0, n1, w.data_ptr(),
+        pr, heads, n0, n1 = c0.shape[0], c0.shape[1], c0.shape[2], c1.shape[2]
+        out = torch.empty((1, pr * (n0 + n1), w.shape[0]), dtype=x.dtype, device=x.device)
+        st = _lib.load().lg_linear_cat(x.data_ptr(), c0.data_ptr(), c1.data_ptr(), heads, n0, n1, pr, w.data_ptr(),
                                        b.data_ptr(), w.shape[0], out.data_ptr(), _Hip._stream(x))
         _check(st, "lg_linear_cat")
         return out
 
     @staticmethod
     def linear_qkv_rotary(x, w_perm, b_perm, cos, sin, heads, splits):
-        n0, n1 = splits
-        mk = lambda n: torch.empty((1, heads, n, 64), dtype=x.dtype, device=x.device)  # noqa: E731
+        n0, n1, pr = _sp(splits)
+        mk = lambda n: torch.empty((pr, heads, n, 64), dtype=x.dtype, device=x.device)  # noqa: E731
         out = [tuple(mk(n) for _ in range(3)) for n in (n0, n1)]
         st = _lib.load().lg_linear_qkv_rotary(x.data_ptr(), w_perm.data_ptr(), b_perm.data_ptr(), cos.data_ptr(),
-                                              sin.data_ptr(), heads, n0, n1, x.shape[2],
+                                              sin.data_ptr(), heads, n0, n1, pr, x.shape[2],
                                               *(t.data_ptr() for t in out[0]), *(t.data_ptr() for t in out[1]),
                                               _Hip._stream(x))
         _check(st, "lg_linear_qkv_rotary")
@@ -128,19 +135,19 @@ class _Hip:
 
     @staticmethod
     def linear_split2(x, w, b, heads, splits):
-        n0, n1 = splits
-        mk = lambda n: torch.empty((1, heads, n, 64), dtype=x.dtype, device=x.device)  # noqa: E731
+        n0, n1, pr = _sp(splits)
+        mk = lambda n: torch.empty((pr, heads, n, 64), dtype=x.dtype, device=x.device)  # noqa: E731
         a0, a1, b0, b1 = mk(n0), mk(n1), mk(n0), mk(n1)
-        st = _lib.load().lg_linear_split2(x.data_ptr(), w.data_ptr(), b.data_ptr(), heads, n0, n1, x.shape[2],
+        st = _lib.load().lg_linear_split2(x.data_ptr(), w.data_ptr(), b.data_ptr(), heads, n0, n1, pr, x.shape[2],
                                           a0.data_ptr(), a1.data_ptr(), b0.data_ptr(), b1.data_ptr(), _Hip._stream(x))
         _check(st, "lg_linear_split2")
         return (a0, a1), (b0, b1)
 
     @staticmethod
     def merge_heads(x0, x1):
-        heads, n0, n1 = x0.shape[1], x0.shape[2], x1.shape[2]
-        out = torch.empty((1, n0 + n1, heads * 64), dtype=x0.dtype, device=x0.device)
-        st = _lib.load().lg_merge_heads(_DT[x0.dtype], x0.data_ptr(), x1.data_ptr(), heads, n0, n1, out.data_ptr(),
+        pr, heads, n0, n1 = x0.shape[0], x0.shape[1], x0.shape[2], x1.shape[2]
+        out = torch.empty((1, pr * (n0 + n1), heads * 64), dtype=x0.dtype, device=x0.device)
+        st = _lib.load().lg_merge_heads(_DT[x0.dtype], x0.data_ptr(), x1.data_ptr(), heads, n0, n1, pr, out.data_ptr(),
                                         _Hip._stream(x0))
         _check(st, "lg_merge_heads")
         return out
@@ -156,12 +163,13 @@ class _Hip:
 
     @staticmethod
     def log_double_softmax(sim, z0, z1):
-        m, n = sim.shape[1], sim.shape[2]
+        """sim [P, m, n], z0 [P, m, 1], z1 [P, n, 1] (P pairs, one launch)."""
+        pr, m, n = sim.shape[0], sim.shape[1], sim.shape[2]
         lib = _lib.load()
         out = torch.empty_like(sim)
         stream = _Hip._stream(sim)
-        ws = _workspace(sim.device, stream, lib.lg_log_double_softmax_workspace(m, n))
-        st = lib.lg_log_double_softmax(sim.data_ptr(), z0.data_ptr(), z1.data_ptr(), m, n, out.data_ptr(),
+        ws = _workspace(sim.device, stream, lib.lg_log_double_softmax_workspace(m, n, pr))
+        st = lib.lg_log_double_softmax(sim.data_ptr(), z0.data_ptr(), z1.data_ptr(), m, n, pr, out.data_ptr(),
                                        ws.data_ptr(), stream)
         _check(st, "lg_log_double_softmax")
         return out
@@ -283,7 +291,7 @@ class SelfBlock(nn.Module):
         q = _rotary(t[0], cos, sin)
         k = _rotary(t[1], cos, sin)
         out, a = [], 0
-        for ni in splits:
+        for ni in splits[:2]:
             out.append(tuple(u[:, a:a + ni].unsqueeze(0).contiguous() for u in (q, k, t[2])))
             a += ni
         return out
@@ -311,7 +319,7 @@ class CrossBlock(nn.Module):
         """[1, N0+N1, d] -> per image [1, H, Ni, 64]."""
         h = t[0].view(t.shape[1], self.heads, self.head_dim).transpose(0, 1)
         out, a = [], 0
-        for ni in splits:
+        for ni in splits[:2]:
             out.append(h[:, a:a + ni].unsqueeze(0).contiguous())
             a += ni
         return out
@@ -414,8 +422,13 @@ def filter_matches(scores: torch.Tensor, th: float):
 class LightGlueMatcher(nn.Module):
     """LightGlue(features=None) of the reference with the MI355X attention (lightglue.py:265-353).
 
-    forward(kpts0 [1,M,2], kpts1 [1,N,2], desc0 [1,M,in], desc1 [1,N,in])
-        -> (desc0 [1,M,d], desc1 [1,N,d], log-assignment scores [1,M,N] fp32)"""
+    forward(kpts0 [P,M,2], kpts1 [P,N,2], desc0 [P,M,in], desc1 [P,N,in])
+        -> (desc0 [P,M,d], desc1 [P,N,d], log-assignment scores [P,M,N] fp32)
+
+    P image pairs of equal sizes go through one forward (the reference's pair loop,
+    demo/demo_mono.cpp:194-418, batched): on the hip path every projection, glue kernel and the
+    dual log-softmax runs once on all pairs' rows, and each layer's self / cross attention is one
+    grouped launch of P-batch calls. glue='torch' runs the pairs one by one."""
 
     def __init__(self, n_layers: int = 9, descriptor_dim: int = 256, input_dim: int = 256, num_heads: int = 4,
                  filter_threshold: float = 0.1, attention: Optional[AttnFn] = None, glue: str = "hip") -> None:
@@ -432,24 +445,34 @@ class LightGlueMatcher(nn.Module):
         self.glue = glue
 
     def forward(self, kpts0, kpts1, desc0, desc1):
-        splits = (desc0.shape[1], desc1.shape[1])
-        x = self.input_proj(torch.cat((desc0, desc1), 1))
+        pr, m, n = desc0.shape[0], desc0.shape[1], desc1.shape[1]
         hip = self.glue == "hip"
+        if not hip and pr > 1:  # the framework-op restatement: one pair at a time
+            outs = [self.forward(kpts0[i:i + 1], kpts1[i:i + 1], desc0[i:i + 1], desc1[i:i + 1]) for i in range(pr)]
+            return tuple(torch.cat(t, 0) for t in zip(*outs))
+        splits = (m, n, pr)
+        x = self.input_proj(torch.cat((desc0, desc1), 1))          # [P, M+N, d], pair-major rows
         if hip and not x.is_cuda:
             raise PluginError("LightGlueMatcher(glue='hip') runs on the GPU only (no CPU fallback)")
         cos, sin = self.posenc(torch.cat((kpts0, kpts1), 1).to(x.dtype))
-        cos, sin = cos[0], sin[0]                                  # [1, N0+N1, 64], broadcast over heads
+        rows = pr * (m + n)
+        x = x.reshape(1, rows, x.shape[-1])
+        cos, sin = cos.reshape(1, rows, -1), sin.reshape(1, rows, -1)  # [1, P*(M+N), 64], broadcast over heads
         if hip:
             cos, sin = cos.contiguous(), sin.contiguous()
         for layer in self.transformers:
             x = layer(x, cos, sin, splits, self.attention, hip)
-        d0, d1 = x[:, :splits[0]], x[:, splits[0]:]
+        x = x.view(pr, m + n, x.shape[-1])
+        d0, d1 = x[:, :m], x[:, m:]
         return d0, d1, self.log_assignment[self.n_layers - 1](d0, d1, hip)
 
     def match(self, kpts0, kpts1, desc0, desc1):
-        """forward + filter_matches (the demo's post-processing)."""
+        """forward + filter_matches (the demo's post-processing); for P > 1 pairs a list of
+        (matches, scores), one per pair."""
         _, _, scores = self.forward(kpts0, kpts1, desc0, desc1)
-        return filter_matches(scores, self.filter_threshold)
+        if scores.shape[0] == 1:
+            return filter_matches(scores, self.filter_threshold)
+        return [filter_matches(scores[i:i + 1], self.filter_threshold) for i in range(scores.shape[0])]
 
 
 # --------------------------------------------------------------------------------------------

@@ -258,6 +258,12 @@ SWEEP = json.load(open(os.path.join(GOLD, "matcher_sweep_index.json")))
 # (descriptors / log-scores / relative row and column sums); bounds ~3-4x those.
 SWEEP_TOL = {"float32": (1e-2, 1e-1, 5e-4), "float16": (6e-2, 0.6, 5e-3)}
 SWEEP_RECALL = 0.9
+# |log-score - reference| on the reference's mutual nearest neighbours (every threshold-0 match: the
+# entries that decide matching), ~3x the largest error observed on MI355X over the sweep sizes
+# (printed by the tests, round 4): fp32 2.0e-2, fp16 0.16 for one pair per forward; inside a batch
+# of pairs the attention launches take other plans (the streaming kernel) and fp16 reaches 0.28
+SWEEP_TOL_MATCHED = {"float32": 6e-2, "float16": 0.5}
+SWEEP_TOL_MATCHED_BATCHED = {"float32": 6e-2, "float16": 0.85}
 
 
 def _sweep_model(name, attention=None, glue="hip"):
@@ -280,9 +286,12 @@ def _check_sweep(g, d0, d1, sc, tol_d, tol_s, tol_rowsum_rel):
     cs = sc[0].double().sum(0).numpy()
     err_sum = max(float(np.abs(rs - g["scores_row_sums"]).max() / np.abs(g["scores_row_sums"]).max()),
                   float(np.abs(cs - g["scores_col_sums"]).max() / np.abs(g["scores_col_sums"]).max()))
-    print(f"sweep errors: desc {err_d:.3e} scores {err_s:.3e} row/col-sum rel {err_sum:.3e}")
+    # the entries that decide the matches: the reference's mutual nearest neighbours (threshold 0)
+    mi, mj = g["matches_all"][:, 0], g["matches_all"][:, 1]
+    err_m = float((sc[0, mi, mj].double() - torch.from_numpy(np.log(g["mscores_all"].astype(np.float64)))).abs().max())
+    print(f"sweep errors: desc {err_d:.3e} scores {err_s:.3e} row/col-sum rel {err_sum:.3e} matched entries {err_m:.3e}")
     assert err_d <= tol_d and err_s <= tol_s and err_sum <= tol_rowsum_rel
-    return err_d, err_s
+    return err_d, err_s, err_m
 
 
 @pytest.mark.parametrize("name", sorted(SWEEP))
@@ -333,8 +342,144 @@ def test_sweep_gpu_matcher_matches_reference(name, dtype):
         d0, d1, sc = model(*(t.to(dev, dt) for t in pair))
         torch.cuda.synchronize()
     d0, d1, sc = d0.float().cpu(), d1.float().cpu(), sc.float().cpu()
-    _check_sweep(g, d0, d1, sc, *SWEEP_TOL[dtype])
+    _, _, err_m = _check_sweep(g, d0, d1, sc, *SWEEP_TOL[dtype])
+    assert err_m <= SWEEP_TOL_MATCHED[dtype], err_m
     got = _match_set(filter_matches(sc, 0.1)[0].numpy())
     ref = _match_set(g["matches"])
     assert len(ref) >= 50
+    print(f"recall {len(got & ref)} / {len(ref)}")
     assert len(got & ref) >= SWEEP_RECALL * len(ref), (len(got & ref), len(ref))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["float16", "float32"])
+@pytest.mark.parametrize("pairs", [4, 8])
+def test_batched_pairs_equal_single_pair_forwards(pairs, dtype):
+    """P image pairs in one forward (pair-major rows through every projection and glue kernel, one
+    grouped attention launch of P-batch calls per block; lightglue.py:328-353 batched, the demo's
+    pair loop demo_mono.cpp:194-418 folded into the batch): each pair's outputs equal that pair's
+    own forward within the fixture bounds, and the fixture pair inside the batch still matches the
+    reference (BASELINE configs[3]/[4] at 1024 x 1024)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lightglue_amd import matcher
+
+    name = "sweep_l9_1024x1024"
+    meta = SWEEP[name]
+    g = np.load(os.path.join(GOLD, f"{name}.npz"))
+    model, pair = _sweep_model(name)
+    dev = torch.device("cuda:0")
+    dt = getattr(torch, dtype)
+    model = model.to(dev, dt)
+    at = pairs // 2  # the fixture pair's slot in the batch
+    ps = [matcher.synthetic_pair(meta["seed"] + 100 + i, meta["m"], meta["n"], overlap=meta["overlap"])
+          for i in range(pairs)]
+    ps[at] = pair
+    batch = tuple(torch.cat([p[j] for p in ps], 0).to(dev, dt) for j in range(4))
+    with torch.no_grad():
+        bd0, bd1, bsc = model(*batch)
+        singles = [model(*(t.to(dev, dt) for t in p)) for p in ps]
+        torch.cuda.synchronize()
+    assert bsc.shape == (pairs, meta["m"], meta["n"])
+    tol_d, tol_s, _ = SWEEP_TOL[dtype]
+    worst = [0.0, 0.0]
+    for i, (d0, d1, sc) in enumerate(singles):
+        ed = max(float((bd0[i] - d0[0]).abs().max()), float((bd1[i] - d1[0]).abs().max()))
+        es = float((bsc[i] - sc[0]).abs().max())
+        worst = [max(worst[0], ed), max(worst[1], es)]
+        assert ed <= tol_d and es <= tol_s, (i, ed, es)
+    print(f"batched vs single forwards (P={pairs}, {dtype}): desc {worst[0]:.3e} scores {worst[1]:.3e}")
+    d0, d1, sc = (t[at:at + 1].float().cpu() for t in (bd0, bd1, bsc))
+    _, _, err_m = _check_sweep(g, d0, d1, sc, *SWEEP_TOL[dtype])
+    assert err_m <= SWEEP_TOL_MATCHED_BATCHED[dtype], err_m
+    matches = model.match(*batch)
+    assert isinstance(matches, list) and len(matches) == pairs
+    got = _match_set(matches[at][0].cpu().numpy())
+    ref = _match_set(g["matches"])
+    assert len(got & ref) >= SWEEP_RECALL * len(ref), (len(got & ref), len(ref))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["float32", "float16"])
+def test_glue_kernels_with_pairs_equal_per_pair_calls(dtype):
+    """Every pair-aware glue kernel (include/lightglue_glue.h, `pairs`) on P = 3 pairs stacked
+    pair-major gives, for each pair, the bits its own P = 1 call gives; the dual log-softmax on a
+    [P, m, n] batch equals its per-pair launches."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lightglue_amd import matcher as mt
+
+    dt = getattr(torch, dtype)
+    dev = torch.device("cuda:0")
+    gen = torch.Generator().manual_seed(5)
+    rnd = lambda *s: torch.randn(*s, generator=gen).to(dev, dt)  # noqa: E731
+    P, n0, n1, h = 3, 37, 70, 4
+    nt = n0 + n1
+    rows = lambda t, i: t[:, i * nt:(i + 1) * nt].contiguous()  # noqa: E731  pair i's rows
+    with torch.no_grad():
+        qkv = rnd(1, P * nt, 3 * h * 64)
+        ang = rnd(1, P * nt, 32).float()
+        cos = torch.cos(ang).repeat_interleave(2, -1).to(dt).contiguous()
+        sin = torch.sin(ang).repeat_interleave(2, -1).to(dt).contiguous()
+        got = mt._Hip.qkv_rotary_split(qkv, cos, sin, h, (n0, n1, P))
+        for i in range(P):
+            one = mt._Hip.qkv_rotary_split(rows(qkv, i), rows(cos, i), rows(sin, i), h, (n0, n1))
+            for g3, o3 in zip(got, one):
+                for g_, o_ in zip(g3, o3):
+                    assert torch.equal(g_[i:i + 1], o_)
+        a, b = rnd(1, P * nt, h * 64), rnd(1, P * nt, h * 64)
+        (a0, a1), (b0, b1) = mt._Hip.split_heads2(a, b, h, (n0, n1, P))
+        assert a0.shape == (P, h, n0, 64) and a1.shape == (P, h, n1, 64)
+        ab = torch.cat((a, b), -1).contiguous()
+        (c0, c1), (d0_, d1_) = mt._Hip.split_heads2_ld(ab, h, (n0, n1, P))
+        for r, g_ in zip((a0, a1, b0, b1), (c0, c1, d0_, d1_)):
+            assert torch.equal(r, g_)
+        for i in range(P):
+            (e0, e1), (f0, f1) = mt._Hip.split_heads2(rows(a, i), rows(b, i), h, (n0, n1))
+            for g_, o_ in zip((a0, a1, b0, b1), (e0, e1, f0, f1)):
+                assert torch.equal(g_[i:i + 1], o_)
+        assert torch.equal(mt._Hip.merge_heads(a0, a1), a)
+        assert torch.equal(mt._Hip.merge_heads_cat(b, a0, a1), torch.cat((b, a), -1))
+        if dtype == "float16":  # fused projections: per-row math, so the batched rows are bitwise
+            x = rnd(1, P * nt, 256) * 0.5
+            blk = mt.SelfBlock(256, h).to(dev, dt)
+            wq, bq = mt._qkv_perm(blk, dt)
+            got = mt._Hip.linear_qkv_rotary(x, wq, bq, cos, sin, h, (n0, n1, P))
+            w2, b2 = rnd(512, 256) * 0.05, rnd(512) * 0.1
+            (s0, s1), (t0, t1) = mt._Hip.linear_split2(x, w2, b2, h, (n0, n1, P))
+            w3, b3 = rnd(512, 512) * 0.05, rnd(512) * 0.1
+            lc = mt._Hip.linear_cat(x, a0, a1, w3, b3)
+            for i in range(P):
+                one = mt._Hip.linear_qkv_rotary(rows(x, i), wq, bq, rows(cos, i), rows(sin, i), h, (n0, n1))
+                for g3, o3 in zip(got, one):
+                    for g_, o_ in zip(g3, o3):
+                        assert torch.equal(g_[i:i + 1], o_)
+                (u0, u1), (v0, v1) = mt._Hip.linear_split2(rows(x, i), w2, b2, h, (n0, n1))
+                for g_, o_ in zip((s0, s1, t0, t1), (u0, u1, v0, v1)):
+                    assert torch.equal(g_[i:i + 1], o_)
+                assert torch.equal(rows(lc, i), mt._Hip.linear_cat(rows(x, i), a0[i:i + 1].contiguous(),
+                                                                   a1[i:i + 1].contiguous(), w3, b3))
+        sim = rnd(P, 300, 257).float() * 5
+        z0, z1 = rnd(P, 300, 1).float(), rnd(P, 257, 1).float()
+        got = mt._Hip.log_double_softmax(sim, z0, z1)
+        for i in range(P):
+            one = mt._Hip.log_double_softmax(sim[i:i + 1].contiguous(), z0[i:i + 1].contiguous(),
+                                             z1[i:i + 1].contiguous())
+            assert torch.equal(got[i:i + 1], one)
+        torch.cuda.synchronize()
+
+
+def test_torch_glue_runs_pairs_one_by_one():
+    """glue='torch' (the CPU restatement) takes P pairs by looping: the same outputs as P forwards."""
+    from lightglue_amd import matcher
+
+    m = matcher.LightGlueMatcher(n_layers=2, attention=_oracle_attention, glue="torch").eval()
+    m.load_state_dict(matcher.seeded_state_dict(1, 2), strict=True)
+    ps = [matcher.synthetic_pair(s, 40, 33) for s in (1, 2)]
+    batch = tuple(torch.cat([p[j] for p in ps], 0) for j in range(4))
+    with torch.no_grad():
+        got = m(*batch)
+        for i, p in enumerate(ps):
+            one = m(*p)
+            for g_, o_ in zip(got, one):
+                assert torch.equal(g_[i:i + 1], o_)

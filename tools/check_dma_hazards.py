@@ -28,7 +28,9 @@ def disassemble(lib):
     lines = []
     with tempfile.TemporaryDirectory() as d:
         fat = os.path.join(d, "fat.bundle")
-        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", lib], check=True, capture_output=True)
+        # (an explicit output file: objcopy with only an input rewrites it in place)
+        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", lib, os.path.join(d, "copy.so")],
+                       check=True, capture_output=True)
         data = open(fat, "rb").read()
         magic = b"__CLANG_OFFLOAD_BUNDLE__"
         starts = [m.start() for m in re.finditer(re.escape(magic), data)]
