@@ -306,3 +306,22 @@ def test_stream_mode_grouped_with_one_tile_calls(dev, oracle_mod, stream_mode):
             ref = _oracle_rows(oracle_mod, q16[bsel], k16[bsel], v16[bsel], rows)
             d = _maxdiff(got[bsel][:, :, rows], ref)
             assert d <= tol, (q16.shape, k16.shape, out_dt, d)
+
+
+@pytest.mark.parametrize("waves,batch", [(8, 32), (8, 12), (4, 24), (4, 32)])
+def test_stream_kernel_bitwise_repeatable(waves, batch, dev):
+    """Ten launches of one forced form give identical bits (the K/V ring's barrier schedule leaves
+    no read of a slot racing a refill: a race shows up as launch-to-launch differences)."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    qn, kn, vn = synth.qkv(5150, 1024, 1024, batch=batch)
+    q, k, v = (_t(x, dev, torch.float16) for x in (qn, kn, vn))
+    ws = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    first = torch.empty_like(q)
+    _launch(lib, q, k, v, first, ws=ws, waves=waves)
+    o = torch.empty_like(q)
+    for _ in range(9):
+        _launch(lib, q, k, v, o, ws=ws, waves=waves)
+        torch.cuda.synchronize()
+        assert torch.equal(o, first)
