@@ -244,14 +244,16 @@ const char* mha_hd64_build_info(void);           /* target arch, compiler, kerne
  * plugin host, no stability promise) ---- */
 /* Launch with a forced kernel form: q_waves/kv_waves/splits as the planner's fields (0 = the
  * planner's choice); q_waves 21 / 22 / 23 force the 32-row / 16-row single-pass kernel / the
- * streaming kernel. phase_mask: 1 main kernel only, 2 combine only, 3 both. Returns a status
+ * streaming kernel (with q_waves 23, kv_waves 4 or 8 picks its 4- or 8-wave form, 0 the planner's).
+ * phase_mask: 1 main kernel only, 2 combine only, 3 both. Returns a status
  * (BAD_PARAM when the form is not compiled for the shape). */
 int32_t mha_hd64_launch_forced(const void* q, const void* k, const void* v, void* o, int32_t batch, int32_t heads,
                                int32_t nq, int32_t nkv, int32_t in_f32, int32_t out_f32, int32_t q_waves,
                                int32_t kv_waves, int32_t splits, void* workspace, size_t ws_bytes,
                                hipStream_t stream, int32_t phase_mask);
 /* The planner's choice for a fp16 call: out4 = {q_waves (or 21/22/23), kv_waves, splits,
- * tiles_per_split}; returns the workspace bytes that plan uses. */
+ * tiles_per_split} (streaming plan: {23, 4 or 8 waves, 1, ...}); returns the workspace bytes that
+ * plan uses. */
 size_t mha_hd64_plan(int32_t batch, int32_t heads, int32_t nq, int32_t nkv, size_t ws_bytes, int32_t* out4);
 /* Per-workgroup timestamp buffer of -DMHA_STAMPS diagnostic builds (ignored by release builds). */
 void mha_hd64_set_stamp_buffer(void* p);

@@ -14,9 +14,12 @@
 // ≈2660 cycles (in-kernel stamps, profiles/r04/stream_stamps.jsonl): item-seam logic inside
 // every step (first / last / seam / tail-mask branches) made the compiler split the step into
 // many blocks, sink the row max out of the MFMA interleave and copy state at the joins. Here:
-//  * item = (call, batch·head, 128-row query block) with ALL of its keys; workgroup = 4 waves,
-//    one per SIMD, 32 query rows each; 80 KiB LDS, <= 256 VGPRs: two workgroups per CU, so every
-//    SIMD runs one wave of each;
+//  * item = (call, batch·head, 32·NW-row query block) with ALL of its keys; workgroup = NW waves,
+//    32 query rows each, <= 256 VGPRs. NW = 4: 128-row items, 80 KiB LDS, two workgroups per CU,
+//    so every SIMD runs one wave of each; NW = 8: 256-row items, 160 KiB LDS, one workgroup per
+//    CU whose two waves per SIMD share every K/V tile (half the DMA per wave, no second workgroup
+//    losing issue arbitration to the first). The planner takes NW = 8 when its last round of
+//    items is at least 3/4 full;
 //  * persistent and XCD-aware: grid = min(items, 512); the workgroups of XCD x walk a contiguous
 //    range of items (consecutive query blocks of one head: its K/V is read through one L2);
 //  * the pipeline runs across items without a seam: an item's LAST step computes QKᵀ of the next
@@ -37,16 +40,19 @@
 //    the start of step t from the max of the previous step, O and l follow after P·V of tile t−1
 //    (which is still at the old max: cdna_hip_programming.md T13's safe order);
 //  * K and V stream by LDS-DMA (`buffer_load_dwordx4 … lds`, 1 KiB per wave instruction, XOR
-//    swizzles applied on the source address) into a 4-slot ring of 64-key tiles (slot = global
-//    tile index mod 4, a runtime value: one scalar add per DMA, one vector add per fragment base),
-//    two tiles ahead and CONTINUOUSLY across items: the last two steps of an item load the next
-//    item's first tiles. Each wave DMAs its own 32 Q rows of the next item during the first step,
-//    so no wave waits for another's Q;
+//    swizzles applied on the source address) into a ring of 64-key tiles (NW 4: 4 slots, 2 tiles
+//    ahead; NW 8: 8 slots, 4 ahead; slot = global tile index mod slots, a runtime value: one
+//    scalar add per DMA, one vector add per fragment base), CONTINUOUSLY across items: a loader
+//    cursor (StreamLoader) runs `lead` tiles ahead of the compute side, into the next item (or
+//    several short ones). Each wave DMAs its own 32 Q rows of the next item during the first
+//    step, so no wave waits for another's Q;
 //  * epilogue per item: 1/l, fp16 pack, v_permlane32_swap pairs → 16-B row-segment stores
 //    (cdna_hip_programming.md T21); rows past nq and keys past nkv are bounded by the buffer
 //    descriptors (no pad / unpad).
-// The DMA is inline asm with hand-counted waits (lds_dma16, mha_hd64_device.h): every step ends
-// with this wave's DMAs landed (vmcnt(0)) and one workgroup barrier.
+// The DMA is inline asm with hand-counted waits (lds_dma16 / lds_dma16_s, mha_hd64_device.h;
+// wait states audited on the built library by tools/check_dma_hazards.py): in the 4-wave form
+// every step ends with this wave's DMAs landed (vmcnt(0)) and one workgroup barrier; in the 8-wave
+// form every second step ends with all but the newest tile's DMAs landed and one barrier.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
