@@ -232,16 +232,21 @@ constexpr float kEmptyMax = -30000.f;  // tile max below this: every key of the 
 // reference's math gives such a row. Returns the mask of the wave's 32 queries that are bad
 // (wave-uniform). Integer tests only: the kernels are built with -fno-honor-nans.
 __device__ __forceinline__ unsigned q_nonfinite_fix(f16x8 (&q)[4]) {
-    float s = 0.f;  // the sum of 32 finite fp16 values is finite (|s| <= 32 * 65504)
+    // the sum of 32 finite fp16 values is finite (|s| <= 32 * 65504); four independent chains
+    // (one per fragment), so the check is 4 dependent dot2 deep instead of 16
+    float ps[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         // (h2 built element-wise: a bit_cast of a vector element w[j] here compiles to w[0] four
         // times with this compiler)
         typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        ps[i] = 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            s = __builtin_amdgcn_fdot2(h2{q[i][2 * j], q[i][2 * j + 1]}, h2{(_Float16)1.f, (_Float16)1.f}, s, false);
+            ps[i] = __builtin_amdgcn_fdot2(h2{q[i][2 * j], q[i][2 * j + 1]}, h2{(_Float16)1.f, (_Float16)1.f}, ps[i],
+                                           false);
     }
+    const float s = (ps[0] + ps[1]) + (ps[2] + ps[3]);
     // the bits through an asm move: on a bit-cast float the compiler reads this test as an
     // fp-class test and, under -fno-honor-nans, drops its NaN half
     unsigned bits;

@@ -338,12 +338,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
     f16x8 pA[2][2], pB[2][2];   // P (fp16) of a tile: B operand of k-step (jj, ss) of Oᵀ = Vᵀ·Pᵀ
 
     // kernel prologue: the first item's Q and global tiles 0 .. L − 1 issued; Q and tiles 0, 1
-    // landed everywhere (NW 8: tiles 2, 3 stay in flight; the first item's FIRST step waits for
-    // tile 2 before its barrier); the V image of the last slot and pB zeroed: the first FIRST step's
+    // landed everywhere (NW 8: tiles 2, 3 issued after the first barrier and still in flight; the
+    // first item's FIRST step waits for tile 2 before its barrier); the V image of the last slot and pB zeroed: the first FIRST step's
     // P·V of "tile −1" adds 0·0 (that slot's first refill is tile kSM, issued after a barrier)
+    // (NW 8: tiles 0, 1 with Q, tiles 2, 3 after the first barrier: the whole chip's burst before
+    // the first barrier is smaller; 16 calls 24.5 vs 25.3 us, profiles/r04/stream_prologue_split.jsonl)
+    constexpr int L0 = NW == 8 ? 2 : L;
     issue_q(cur);
 #pragma unroll
-    for (int i = 0; i < L; ++i) {
+    for (int i = 0; i < L0; ++i) {
         issue_tile((unsigned)i);
         ld_advance();
     }
@@ -355,8 +358,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) pB[jj][ss] = f16x8{};
     // Q and tile 0 first: tile 0's QKᵀ below runs while tile 1 lands
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L - 1) * kPiece) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((L0 - 1) * kPiece) : "memory");
     __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int i = L0; i < L; ++i) {
+        issue_tile((unsigned)i);
+        ld_advance();
+    }
 #ifdef MHA_STREAM_STAMPS
     SCLK(ck_pro);
     ck_last = ck_pro;

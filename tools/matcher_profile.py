@@ -1,4 +1,9 @@
-"""Diagnostic driver for rocprofv3: eager fp16 LightGlue matcher forwards at N keypoints."""
+"""Diagnostic: the end-to-end fp16 matcher with P image pairs per forward (bench.py
+matcher_batched_pairs' form), replayed from a graph, for a kernel trace:
+
+    rocprofv3 --kernel-trace --stats -d <dir> -- python tools/matcher_profile.py [P] [n] [reps]
+
+Prints ms per forward and pairs/s (HIP events)."""
 import os
 import sys
 
@@ -8,13 +13,38 @@ import torch  # noqa: E402
 
 from lightglue_amd import matcher  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-dev = torch.device("cuda:0")
-model = matcher.LightGlueMatcher(n_layers=9).eval()
-model.load_state_dict(matcher.seeded_state_dict(7, 9), strict=True)
-model = model.to(dev, torch.float16)
-k0, k1, d0, d1 = (t.to(dev, torch.float16) for t in matcher.synthetic_pair(40, n, n))
-with torch.no_grad():
-    for _ in range(12):
-        model(k0, k1, d0, d1)
-torch.cuda.synchronize()
+
+def main():
+    P = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    dev = torch.device("cuda:0")
+    model = matcher.LightGlueMatcher(n_layers=9).eval()
+    model.load_state_dict(matcher.seeded_state_dict(7, 9), strict=True)
+    model = model.to(dev, torch.float16)
+    ps = [matcher.synthetic_pair(80 + i, n, n) for i in range(P)]
+    batch = tuple(torch.cat([p[j] for p in ps], 0).to(dev, torch.float16) for j in range(4))
+    st = torch.cuda.Stream(dev)
+    with torch.no_grad(), torch.cuda.stream(st):
+        for _ in range(2):
+            model(*batch)
+        st.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            out = model(*batch)
+    g.replay()
+    st.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    with torch.cuda.stream(st):
+        for _ in range(reps):
+            g.replay()
+    e1.record(st)
+    st.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    assert bool(torch.isfinite(out[2]).all())
+    print(f"P={P} n={n}: {ms:.4f} ms per forward, {P * 1e3 / ms:.1f} pairs/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

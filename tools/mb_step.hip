@@ -22,6 +22,8 @@
 //           the K/V stream: 2 DMA pieces per wave and step)
 // 4096 ROT  (NW = 8) waves 4..7 run each step's phase B before its phase A: the two waves of a SIMD
 //           (w, w + 4) are in different phases between barriers
+// 8192 VSUM  row sums on the vector pipe instead of RSUM's MFMAs: 16 v_dot2c_f32_f16 of the packed P
+//           per step (four chains), two beside each P·V MFMA
 // 512 POLY   half of the exponentials as a degree-3 exp2 polynomial on the
 //           packed-FMA path (v_pk_fma_f32 + exponent insert) instead of v_exp_f32
 // Prints per variant: µs per launch (HIP events, median of 5 launches), TFLOP/s (the step's useful
@@ -42,7 +44,7 @@
 using namespace mha_hd64;
 
 enum : int { EXP = 1, CVT = 2, MAX = 4, RSUM = 8, LDSK = 16, LDSV = 32, DMA = 64, BAR = 128, SCHK = 256, POLY = 512,
-              BAR2 = 1024, WAIT0 = 2048, ROT = 4096 };
+              BAR2 = 1024, WAIT0 = 2048, ROT = 4096, VSUM = 8192 };
 constexpr int ITER = 1024;  // steps per wave (2 x this many tiles per loop trip)
 constexpr int kSlot = 2 * kTileBytes;
 constexpr int kSlots = 4;
@@ -113,6 +115,7 @@ __global__ __launch_bounds__(64 * NW, RB == 1 ? 2 : 1) void kern(const f16* src,
     for (int b = 0; b < RB; ++b) cm[b] = splat16(-3.f);
     f32x16 o[RB][2] = {};
     f32x4 l[RB] = {};
+    float vs[RB][4] = {};
     f32x16 sA[RB][2], sB[RB][2];
     f16x8 pA[RB][4], pB[RB][4];
 #pragma unroll
@@ -247,8 +250,20 @@ __global__ __launch_bounds__(64 * NW, RB == 1 ? 2 : 1) void kern(const f16* src,
                 o[b][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa[jj][ss], pp_[b][k], o[b][0], 0, 0, 0);
                 fill(g++);
                 __builtin_amdgcn_sched_barrier(0);
+                if (F & VSUM) {
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        vs[b][k] = __builtin_amdgcn_fdot2(h2{pp_[b][k][2 * j], pp_[b][k][2 * j + 1]}, h2{(f16)1.f, (f16)1.f},
+                                                          vs[b][k], false);
+                }
                 o[b][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb[jj][ss], pp_[b][k], o[b][1], 0, 0, 0);
                 fill(g++);
+                if (F & VSUM) {
+#pragma unroll
+                    for (int j = 2; j < 4; ++j)
+                        vs[b][k] = __builtin_amdgcn_fdot2(h2{pp_[b][k][2 * j], pp_[b][k][2 * j + 1]}, h2{(f16)1.f, (f16)1.f},
+                                                          vs[b][k], false);
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 if (F & RSUM) {
                     l[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, pp_[b][k], l[b], 0, 0, 0);
@@ -326,7 +341,7 @@ __global__ __launch_bounds__(64 * NW, RB == 1 ? 2 : 1) void kern(const f16* src,
     for (int b = 0; b < RB; ++b) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc += o[b][0][i] + o[b][1][i] + sA[b][0][i] + sB[b][1][i];
-        acc += l[b][0] + l[b][1];
+        acc += l[b][0] + l[b][1] + vs[b][0] + vs[b][1] + vs[b][2] + vs[b][3];
 #pragma unroll
         for (int k = 0; k < 4; ++k) acc += (float)pA[b][k][0] + (float)pB[b][k][1];
     }
@@ -423,6 +438,10 @@ int main(int argc, char** argv) {
         row<1, 8, VECS | LDSK | LDSV | DMA | BAR>("j' 8 waves, sum check", filt, src, out, clk);
         row<1, 8, VECS | LDSK | LDSV | DMA | BAR | BAR2>("j2 8 waves, sum check, bar / 2", filt, src, out, clk);
         row<1, 8, VECS | LDSK | LDSV | DMA>("j3 8 waves, sum check, no bar", filt, src, out, clk);
+        row<1, 8, VEC | LDSK | LDSV | DMA | BAR | BAR2>("j4 8 waves, full step, bar / 2 (the kernel's form)", filt, src, out, clk);
+        row<1, 8, (VEC & ~RSUM) | VSUM | LDSK | LDSV | DMA | BAR | BAR2>("j5 8 waves, bar / 2, VALU row sums", filt, src, out, clk);
+        row<1, 4, (VEC & ~RSUM) | VSUM | LDSK | LDSV | DMA | BAR>("h3 full step, VALU row sums", filt, src, out, clk);
+        row<1, 4, (VEC & ~RSUM) | VSUM>("e3 all vector work, VALU row sums", filt, src, out, clk);
         row<1, 8, VEC | LDSK | LDSV | DMA | BAR | ROT>("k  8 waves, full step, rotated", filt, src, out, clk);
         row<1, 8, VECS | LDSK | LDSV | DMA | BAR | ROT>("k' 8 waves, sum check, rotated", filt, src, out, clk);
         row<1, 8, VECS | LDSK | LDSV | DMA | BAR | BAR2 | ROT>("k2 8 waves, sum check, bar / 2, rot", filt, src, out, clk);

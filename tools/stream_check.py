@@ -113,14 +113,70 @@ def timing(lib, dev, quick):
         print(json.dumps(out), flush=True)
 
 
+def slope(libs, dev, waves=(4, 8)):
+    """Per-step cost without item seams: one item per workgroup (B = 16 calls of nq = 1024: 256
+    items of 256 rows / 512 of 128 rows = one residency round), nkv = 1024 .. 8192; the slope of
+    launch time over 64-key steps is the steady step, the intercept the launch's fixed cost. Also
+    B = 32 and 64 at nkv = 1024 (2 and 4 items per workgroup). Libraries and forms interleaved."""
+    stream = torch.cuda.Stream()
+    ws = torch.empty(5242880, dtype=torch.uint8, device=dev)
+    K = 20
+    nkvs = (1024, 2048, 4096, 8192)
+    cfgs = [(16, n) for n in nkvs] + [(32, 1024), (64, 1024)]
+    data = {}
+    for B, n in cfgs:
+        data[(B, n)] = (torch.randn(B, 4, 1024, 64, device=dev).half(), torch.randn(B, 4, n, 64, device=dev).half(),
+                        torch.randn(B, 4, n, 64, device=dev).half(), torch.empty(B, 4, 1024, 64, device=dev).half())
+    graphs = {}
+    for li, lib in enumerate(libs):
+        for w in waves:
+            for B, n in cfgs:
+                q, k, v, o = data[(B, n)]
+                with torch.cuda.stream(stream):
+                    forced(lib, q, k, v, o, STREAM, ws, stream, w)
+                    gr = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gr, stream=stream):
+                        for _ in range(K):
+                            forced(lib, q, k, v, o, STREAM, ws, stream, w)
+                graphs[(li, w, B, n)] = gr
+    torch.cuda.synchronize()
+    times = {key: [] for key in graphs}
+    for _ in range(7):
+        for key, gr in graphs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(stream):
+                e0.record(stream)
+                gr.replay()
+                e1.record(stream)
+            e1.synchronize()
+            times[key].append(e0.elapsed_time(e1) * 1e3 / K)
+    for li in range(len(libs)):
+        for w in waves:
+            us = [statistics.median(times[(li, w, 16, n)]) for n in nkvs]
+            steps = [n // 64 for n in nkvs]
+            mx, my = statistics.mean(steps), statistics.mean(us)
+            b = sum((x - mx) * (y - my) for x, y in zip(steps, us)) / sum((x - mx) ** 2 for x in steps)
+            extra = {f"b{B}_us": round(statistics.median(times[(li, w, B, 1024)]), 3) for B in (32, 64)}
+            extra.update({f"b{B}_frac": round(4.0 * B * 4 * 1024 * 1024 * 64 / (extra[f"b{B}_us"] * 1e-6) / 2.5e15, 4)
+                          for B in (32, 64)})
+            print(json.dumps({"lib": li, "waves": w, "b16_us": [round(u, 3) for u in us], "nkv": list(nkvs),
+                              "us_per_step": round(b, 4), "intercept_us": round(my - b * mx, 3),
+                              "b16_frac": round(4.0 * 16 * 4 * 1024 * 1024 * 64 / (us[0] * 1e-6) / 2.5e15, 4),
+                              **extra}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--lib", default=_lib.LIB_PATH)
     ap.add_argument("--no-timing", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--slope", default=None, help="comma-separated libraries: per-step slope of each (A/B)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
+    if args.slope:
+        slope([load(p) for p in args.slope.split(",")], dev)
+        return
     lib = load(args.lib)
     if not args.no_parity:
         parity(lib, dev, args.quick)
