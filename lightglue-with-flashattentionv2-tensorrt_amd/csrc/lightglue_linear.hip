@@ -23,6 +23,9 @@
 // landed (counted vmcnt + barrier) while the later chunks stream in.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+#include <atomic>
 
 #include "lightglue_glue.h"
 #include "mha_hd64.h"
@@ -207,8 +210,198 @@ __global__ __launch_bounds__(256) void linear_kernel(LinArgs p) {
     }
 }
 
+// ---- the wide form, for launches with many rows (several image pairs per forward) ----
+// Workgroup: 256 rows (m) x 128 output channels (n) a tile, persistent over tiles (the DMA ring
+// runs on across tile seams: the next tile's first two K steps load during the current tile's
+// last two), 8 waves as 4 (m) x 2 (n) tiles of 64 x 64
+// (2 x 2 MFMA blocks of 32 x 32 each); K in 64-deep steps through a 3-stage LDS-DMA ring (48 KiB a
+// stage: W [128 rows][128 B] + A [256 rows][128 B], 16-B units XOR-swizzled by (row >> 1) & 7 on
+// the source address: conflict-free ds_read_b128 in every lane group), two steps in flight. Per
+// step and wave: 16 MFMA beside 16 fragment reads. The k16 blocks enter each accumulator in the
+// same order as in linear_kernel, so both forms give the same bits. Against the 64 x 64 form it
+// moves a quarter of the operand bytes per MAC out of L2 (128 KiB per 64 x 64 x 512 tile there).
+constexpr int kWM = 256, kWN = 128, kWK = 64;
+constexpr int kWStage = (kWM + kWN) * kWK * 2;  // 48 KiB
+constexpr int kWStages = 3;
+constexpr int kWGrid = 256;  // one workgroup per CU
+
+template <int EPI, bool GATHER, int KS>
+__global__ __launch_bounds__(512, 1) void linear_wide_kernel(LinArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[kWStages * kWStage];  // 144 KiB
+    lds_char* const lds = (lds_char*)smem;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave & 3, wn = wave >> 2;  // this wave's 64 x 64 tile of the 256 x 128
+    const int r = lane & 31, hh = lane >> 5;
+    // Persistent and XCD-aware: the workgroups of XCD x walk the contiguous tile range [jb, je)
+    // (tile j = m tile j / ntiles, n tile j % ntiles: the n tiles of one m tile run side by side
+    // on one XCD, so their A tile is read through one L2), every G-th tile from their local index.
+    const int T = p.total, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int q8 = T >> 3, r8 = T & 7;
+    const int jb = xcd * q8 + min(xcd, r8), je = jb + q8 + (xcd < r8 ? 1 : 0);
+    const int G = ((int)gridDim.x - xcd + 7) >> 3;
+    const int ntiles = p.n / kWN;
+    const int j0 = jb + loc;
+    if (j0 >= je) return;
+    const int ntile_w = (je - j0 + G - 1) / G;  // tiles of this workgroup
+    const int nsteps = ntile_w * KS;            // K steps over all of them
+
+    // DMA of global step gs (tile gs / KS, K step gs % KS) into stage st: W pieces wave, wave + 8
+    // (16 x 8 rows), A pieces wave + 8i (32 x 8 rows); lane -> (row 8i + lane / 8, LDS unit
+    // lane % 8 <- global unit (lane % 8) ^ ((row >> 1) & 7))
+    auto issue = [&](int gs, int st) {
+        const int jt = j0 + G * (gs / KS), ks = gs % KS;
+        const int mt = jt / ntiles, m0 = mt * kWM, n0 = (jt - mt * ntiles) * kWN;
+        char* const sb = smem + st * kWStage;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = wave + 8 * h, row = 8 * i + (lane >> 3);
+            const int gc = ks * (kWK / 8) + ((lane & 7) ^ ((row >> 1) & 7));
+            const int wr = min(n0 + row, p.n - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(p.w + (size_t)wr * p.k + gc * 8),
+                                             (__attribute__((address_space(3))) void*)(sb + i * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const int i = wave + 8 * h, row = 8 * i + (lane >> 3);
+            const int gc = ks * (kWK / 8) + ((lane & 7) ^ ((row >> 1) & 7));
+            const int ar = min(m0 + row, p.m - 1);
+            __builtin_amdgcn_global_load_lds((const void*)a_src<GATHER>(p, ar, gc),
+                                             (__attribute__((address_space(3))) void*)(sb + kWN * 128 + i * 1024), 16,
+                                             0, 0);
+        }
+    };
+    issue(0, 0);
+    if (nsteps > 1) issue(1, 1);
+
+    unsigned wro[2], aro[2];  // per block: row offset and swizzle key of this lane's fragment row
+    int wsw[2], asw[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int wrow = wn * 64 + 32 * b + r, arow = wm * 64 + 32 * b + r;
+        wro[b] = (unsigned)(wrow * 128), wsw[b] = (wrow >> 1) & 7;
+        aro[b] = (unsigned)(kWN * 128 + arow * 128), asw[b] = (arow >> 1) & 7;
+    }
+    int st = 0;  // stage of global step gs
+    for (int t = 0; t < ntile_w; ++t) {
+        const int jt = j0 + G * t;
+        const int mt = jt / ntiles, m0 = mt * kWM, n0 = (jt - mt * ntiles) * kWN;
+        f32x16 acc[2][2] = {};  // [n block][m block]
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int gs = t * KS + ks;
+            // step gs landed for this wave's 6 DMAs (step gs + 1's stay in flight), then for
+            // everyone's; after this barrier every wave is past step gs − 1, so its stage takes
+            // step gs + 2 (lgkmcnt(0): this wave's fragment reads of step gs − 1 are done)
+            if (gs + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (gs + 2 < nsteps) issue(gs + 2, st == 0 ? 2 : st - 1);
+            const unsigned sb = (unsigned)(st * kWStage);
+            st = st == 2 ? 0 : st + 1;
+#pragma unroll
+            for (int s = 0; s < kWK / 16; ++s) {
+                f16x8 wf[2], af[2];
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const int u = 2 * s + hh;
+                    wf[b] = *(lds_f16x8*)(lds + sb + wro[b] + ((u ^ wsw[b]) << 4));
+                    af[b] = *(lds_f16x8*)(lds + sb + aro[b] + ((u ^ asw[b]) << 4));
+                }
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+                    for (int mb = 0; mb < 2; ++mb)
+                        acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[nb], af[mb], acc[nb][mb], 0, 0, 0);
+            }
+        }
+
+        // ---- epilogue: per (n block, m block), lane = activation row; acc[.][.][4g + t] =
+        // channel n0 + wn*64 + 32 nb + 8g + 4hh + t (the 64 x 64 form's epilogue per 32 x 32
+        // block). Its operand loads return after the next tile's first two DMA steps (issued
+        // above): the wait for them is the wait the next tile's first step makes anyway. ----
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const int row = m0 + wm * 64 + 32 * mb + r;
+            if (row >= p.m) continue;
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int n = n0 + wn * 64 + 32 * nb + 8 * g + 4 * hh;
+                    const f16x4 b4 = *reinterpret_cast<const f16x4*>(p.bias + n);
+                    float v[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] = acc[nb][mb][4 * g + u] + (float)b4[u];
+                    if constexpr (EPI == EPI_BIAS) {
+                        if (p.res) {
+                            const f16x4 rr = *reinterpret_cast<const f16x4*>(p.res + (size_t)row * p.n + n);
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) v[u] += (float)rr[u];
+                        }
+                        *reinterpret_cast<f16x4*>(p.out[0] + (size_t)row * p.n + n) =
+                            f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+                    } else {
+                        const int hd = p.heads * kD;
+                        const int part = n / hd, h = (n % hd) / kD, d = n % kD;
+                        const LinRow lr = lin_row(p, row, h);
+                        if constexpr (EPI == EPI_QKV_ROTARY) {
+                            if (part < 2) {
+                                const f16x4 cc = *reinterpret_cast<const f16x4*>(p.cosv + (size_t)row * kD + d);
+                                const f16x4 ss = *reinterpret_cast<const f16x4*>(p.sinv + (size_t)row * kD + d);
+#pragma unroll
+                                for (int u = 0; u < 4; u += 2) {
+                                    const float x0 = v[u], x1 = v[u + 1];
+                                    v[u] = x0 * (float)cc[u] - x1 * (float)ss[u];
+                                    v[u + 1] = x1 * (float)cc[u + 1] + x0 * (float)ss[u + 1];
+                                }
+                            }
+                        }
+                        f16* dst = p.out[(lr.first ? 0 : (EPI == EPI_QKV_ROTARY ? 3 : 1)) +
+                                         (EPI == EPI_QKV_ROTARY ? part : 2 * part)];
+                        *reinterpret_cast<f16x4*>(dst + lr.off + d) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+                    }
+                }
+            }
+        }
+    }
+}
+
+// The wide form where it fills the chip: at least one round of its 256 x 128 tiles (n a multiple of
+// 128). lg_linear_set_wide(0 / 1) or LG_LINEAR_WIDE=0 / 1 forces it off / on (where n allows), for
+// tests and A/B timing; -1 (the default) chooses by size.
+std::atomic<int> g_wide{-2};
+int wide_mode() {
+    int v = g_wide.load();
+    if (v == -2) {
+        const char* e = std::getenv("LG_LINEAR_WIDE");
+        int expect = -2;
+        g_wide.compare_exchange_strong(expect, e ? (e[0] == '1' ? 1 : 0) : -1);
+        v = g_wide.load();
+    }
+    return v;
+}
+bool use_wide(const LinArgs& p) {
+    if (p.n % kWN) return false;
+    const int w = wide_mode();
+    if (w >= 0) return w == 1;
+    return (long)((p.m + kWM - 1) / kWM) * (p.n / kWN) >= 256;
+}
+
 template <int EPI, bool GATHER>
 int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
+    if (use_wide(p)) {
+        p.mtiles = (p.m + kWM - 1) / kWM;
+        p.total = p.mtiles * (p.n / kWN);
+        const int grid = p.total < kWGrid ? p.total : kWGrid;  // persistent: one round
+        if (p.k == 256)
+            hipLaunchKernelGGL((linear_wide_kernel<EPI, GATHER, 4>), dim3(grid), dim3(512), 0, stream, p);
+        else
+            hipLaunchKernelGGL((linear_wide_kernel<EPI, GATHER, 8>), dim3(grid), dim3(512), 0, stream, p);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
+                               : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, what, hipGetErrorString(e));
+    }
     p.mtiles = (p.m + kBM - 1) / kBM;
     p.total = p.mtiles * (p.n / kBN);
     if (p.k == 256)
@@ -287,6 +480,11 @@ int32_t lg_linear_split2(const void* x, const void* w, const void* bias, int32_t
     for (int i = 0; i < 4; ++i) p.out[i] = outs[i];
     p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
     return launch<EPI_SPLIT2, false>(p, stream, "lg_linear_split2");
+}
+
+int32_t lg_linear_set_wide(int32_t mode) {
+    wide_mode();
+    return g_wide.exchange(mode < 0 ? -1 : (mode ? 1 : 0));
 }
 
 }  // extern "C"

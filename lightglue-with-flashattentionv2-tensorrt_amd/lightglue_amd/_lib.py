@@ -137,6 +137,7 @@ SIGNATURES.update({
     "lg_layernorm_gelu": ([_I, _P, _P, _P, _I, _I, ctypes.c_float, _P, _P], _I),
     "lg_log_double_softmax_workspace": ([_I, _I, _I], _S),
     "lg_log_double_softmax": ([_P, _P, _P, _I, _I, _I, _P, _P, _P], _I),
+    "lg_linear_set_wide": ([_I], _I),
     # kernel-form switches (include/mha_hd64.h "kernel-form switches")
     "mha_hd64_set_fused_combine": ([_I], None),
     "mha_hd64_set_f32_inkernel": ([_I], None),

@@ -483,3 +483,55 @@ def test_torch_glue_runs_pairs_one_by_one():
             one = m(*p)
             for g_, o_ in zip(got, one):
                 assert torch.equal(g_[i:i + 1], o_)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pairs,n0,n1", [(3, 37, 70), (2, 1000, 777), (16, 1024, 1024)])
+def test_wide_projections_equal_narrow(pairs, n0, n1):
+    """The projections' 256 x 128-tile form (csrc/lightglue_linear.hip linear_wide_kernel, taken for
+    launches of at least one round of its tiles: several image pairs per forward) gives the bits of
+    the 64 x 64 form on every fused entry point — ragged row counts (rows past m in a tile), both
+    K (256 and 512), residual on and off, the A-gather of lg_linear_cat, the per-image scatters."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lightglue_amd import _lib
+    from lightglue_amd import matcher as mt
+
+    lib = _lib.load()
+    dev, dt, h = torch.device("cuda:0"), torch.float16, 4
+    gen = torch.Generator().manual_seed(11)
+    rnd = lambda *s: torch.randn(*s, generator=gen).to(dev, dt)  # noqa: E731
+    nt = n0 + n1
+    sp = (n0, n1, pairs)
+    with torch.no_grad():
+        x = rnd(1, pairs * nt, 256) * 0.5
+        hx = rnd(1, pairs * nt, 512) * 0.5
+        ang = rnd(1, pairs * nt, 32).float()
+        cos = torch.cos(ang).repeat_interleave(2, -1).to(dt).contiguous()
+        sin = torch.sin(ang).repeat_interleave(2, -1).to(dt).contiguous()
+        c0, c1 = rnd(pairs, h, n0, 64), rnd(pairs, h, n1, 64)
+        blk = mt.SelfBlock(256, h).to(dev, dt)
+        wq, bq = mt._qkv_perm(blk, dt)
+        w2, b2 = rnd(512, 256) * 0.05, rnd(512) * 0.1
+        w3, b3 = rnd(512, 512) * 0.05, rnd(512) * 0.1
+        w4, b4 = rnd(256, 512) * 0.05, rnd(256) * 0.1
+
+        def run():
+            return [mt._Hip.linear_qkv_rotary(x, wq, bq, cos, sin, h, sp),
+                    mt._Hip.linear_split2(x, w2, b2, h, sp),
+                    mt._Hip.linear_cat(x, c0, c1, w3, b3),
+                    mt._Hip.linear(hx, w4, b4, x), mt._Hip.linear(hx, w4, b4)]
+
+        flat = lambda o: [t for t in (o if isinstance(o, torch.Tensor) else  # noqa: E731
+                                      [u for v in o for u in (v if isinstance(v, (tuple, list)) else [v])])]
+        prev = lib.lg_linear_set_wide(0)
+        try:
+            narrow = [flat(o) for o in run()]
+            lib.lg_linear_set_wide(1)
+            wide = [flat(o) for o in run()]
+            torch.cuda.synchronize()
+        finally:
+            lib.lg_linear_set_wide(prev)
+        for a, b in zip(narrow, wide):
+            for ta, tb in zip(a, b):
+                assert torch.equal(ta, tb)

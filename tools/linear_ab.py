@@ -1,0 +1,75 @@
+"""Diagnostic: the matcher projections (include/lightglue_glue.h lg_linear*) in their 64 x 64 and
+256 x 128-tile forms (lg_linear_set_wide 0 / 1) at P image pairs of n keypoints per image, graph
+replay of back-to-back launches, interleaved; TFLOP/s of each.
+
+    python tools/linear_ab.py [P] [n]"""
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "lightglue-with-flashattentionv2-tensorrt_amd")]
+import torch  # noqa: E402
+
+from lightglue_amd import _lib  # noqa: E402
+from lightglue_amd import matcher as mt  # noqa: E402
+
+
+def main():
+    P = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    lib = _lib.load()
+    dev, dt, h = torch.device("cuda:0"), torch.float16, 4
+    M = P * 2 * n
+    sp = (n, n, P)
+    x = torch.randn(1, M, 256, device=dev, dtype=dt) * 0.5
+    hx = torch.randn(1, M, 512, device=dev, dtype=dt) * 0.5
+    cos = torch.randn(1, M, 64, device=dev, dtype=dt)
+    sin = torch.randn(1, M, 64, device=dev, dtype=dt)
+    c0, c1 = torch.randn(P, h, n, 64, device=dev, dtype=dt), torch.randn(P, h, n, 64, device=dev, dtype=dt)
+    w768, b768 = torch.randn(768, 256, device=dev, dtype=dt) * 0.05, torch.randn(768, device=dev, dtype=dt)
+    w2, b2 = torch.randn(512, 256, device=dev, dtype=dt) * 0.05, torch.randn(512, device=dev, dtype=dt)
+    w3, b3 = torch.randn(512, 512, device=dev, dtype=dt) * 0.05, torch.randn(512, device=dev, dtype=dt)
+    w4, b4 = torch.randn(256, 512, device=dev, dtype=dt) * 0.05, torch.randn(256, device=dev, dtype=dt)
+    ops = {
+        "qkv_rotary k256 n768": (lambda: mt._Hip.linear_qkv_rotary(x, w768, b768, cos, sin, h, sp), 256 * 768),
+        "split2 k256 n512": (lambda: mt._Hip.linear_split2(x, w2, b2, h, sp), 256 * 512),
+        "cat k512 n512": (lambda: mt._Hip.linear_cat(x, c0, c1, w3, b3), 512 * 512),
+        "linear+res k512 n256": (lambda: mt._Hip.linear(hx, w4, b4, x), 512 * 256),
+    }
+    st = torch.cuda.Stream(dev)
+    K = 20
+    graphs = {}
+    for name, (fn, _) in ops.items():
+        for wide in (0, 1):
+            lib.lg_linear_set_wide(wide)
+            with torch.cuda.stream(st):
+                fn()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=st):
+                    for _ in range(K):
+                        fn()
+            graphs[(name, wide)] = g
+    lib.lg_linear_set_wide(-1)
+    torch.cuda.synchronize()
+    times = {k: [] for k in graphs}
+    for _ in range(5):
+        for k, g in graphs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(st):
+                e0.record(st)
+                g.replay()
+                e1.record(st)
+            e1.synchronize()
+            times[k].append(e0.elapsed_time(e1) * 1e3 / K)
+    for name, (_, kn) in ops.items():
+        row = {"op": name, "M": M}
+        for wide in (0, 1):
+            us = statistics.median(times[(name, wide)])
+            row["wide" if wide else "narrow"] = {"us": round(us, 2), "tflops": round(2.0 * M * kn / us / 1e6, 1)}
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
