@@ -88,9 +88,10 @@ size_t lg_log_double_softmax_workspace(int32_t m, int32_t n, int32_t batch);
 int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1, int32_t m, int32_t n, int32_t batch,
                               float* scores, void* workspace, hipStream_t stream);
 
-/* Test and benchmark hook: the projections' 256 x 128-tile form (launches of at least one round of
- * those tiles, e.g. several image pairs per forward) forced off (0), on where n allows (1), or
- * chosen by size (-1, the default). Both forms give the same bits. Returns the previous mode. */
+/* Test and benchmark hook: the projections' tile forms for launches of many rows (several image
+ * pairs per forward): 0 the 64 x 64 form only, 1 the 256 x 128 form where n allows, 2 the
+ * 256 x 256 form where n allows, -1 (the default) chosen by size. Every form gives the same bits.
+ * Returns the previous mode. */
 int32_t lg_linear_set_wide(int32_t mode);
 
 #ifdef __cplusplus

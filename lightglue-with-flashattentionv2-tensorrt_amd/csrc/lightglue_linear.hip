@@ -210,6 +210,42 @@ __global__ __launch_bounds__(256) void linear_kernel(LinArgs p) {
     }
 }
 
+// One lane's 4 consecutive output channels n..n+3 of activation row `row` (acc elements 4g..4g+3):
+// bias, then residual (EPI_BIAS) / rotary + per-image head-major scatter / head split.
+template <int EPI>
+__device__ __forceinline__ void epi_store(const LinArgs& p, int row, int n, const f32x16& acc, int g) {
+    const f16x4 b4 = *reinterpret_cast<const f16x4*>(p.bias + n);
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = acc[4 * g + u] + (float)b4[u];
+    if constexpr (EPI == EPI_BIAS) {
+        if (p.res) {
+            const f16x4 rr = *reinterpret_cast<const f16x4*>(p.res + (size_t)row * p.n + n);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] += (float)rr[u];
+        }
+        *reinterpret_cast<f16x4*>(p.out[0] + (size_t)row * p.n + n) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+    } else {
+        const int hd = p.heads * kD;
+        const int part = n / hd, h = (n % hd) / kD, d = n % kD;
+        const LinRow lr = lin_row(p, row, h);
+        if constexpr (EPI == EPI_QKV_ROTARY) {
+            if (part < 2) {
+                const f16x4 cc = *reinterpret_cast<const f16x4*>(p.cosv + (size_t)row * kD + d);
+                const f16x4 ss = *reinterpret_cast<const f16x4*>(p.sinv + (size_t)row * kD + d);
+#pragma unroll
+                for (int u = 0; u < 4; u += 2) {
+                    const float x0 = v[u], x1 = v[u + 1];
+                    v[u] = x0 * (float)cc[u] - x1 * (float)ss[u];
+                    v[u + 1] = x1 * (float)cc[u + 1] + x0 * (float)ss[u + 1];
+                }
+            }
+        }
+        f16* dst = p.out[(lr.first ? 0 : (EPI == EPI_QKV_ROTARY ? 3 : 1)) + (EPI == EPI_QKV_ROTARY ? part : 2 * part)];
+        *reinterpret_cast<f16x4*>(dst + lr.off + d) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+    }
+}
+
 // ---- the wide form, for launches with many rows (several image pairs per forward) ----
 // Workgroup: 256 rows (m) x 128 output channels (n) a tile, persistent over tiles (the DMA ring
 // runs on across tile seams: the next tile's first two K steps load during the current tile's
@@ -367,6 +403,119 @@ __global__ __launch_bounds__(512, 1) void linear_wide_kernel(LinArgs p) {
     }
 }
 
+// ---- the square form: 256 x 256 tiles, K in 32-deep steps through a 4-stage ring (32 KiB a
+// stage: W and A [256 rows][64 B], 16-B units XOR-swizzled by (row >> 2) & 3), three steps in
+// flight; 8 waves as 4 (m) x 2 (n) tiles of 64 rows x 128 channels (2 x 4 MFMA blocks). A step
+// stages 32 KiB for 4.2 MFLOP (the 256 x 128 form: 48 KiB). Same k16 order per accumulator as
+// the other forms: same bits. (lg_linear_set_wide(2) / LG_LINEAR_WIDE=2, where n % 256 == 0.)
+constexpr int kSM_ = 256, kSN = 256, kSK = 32;
+constexpr int kSStage = (kSM_ + kSN) * kSK * 2;  // 32 KiB
+constexpr int kSStages = 4;
+
+template <int EPI, bool GATHER, int KS>
+__global__ __launch_bounds__(512, 1) void linear_sq_kernel(LinArgs p) {
+    __shared__ __attribute__((aligned(16))) char smem[kSStages * kSStage];  // 128 KiB
+    lds_char* const lds = (lds_char*)smem;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave & 3, wn = wave >> 2;  // this wave's 64 x 128 tile of the 256 x 256
+    const int r = lane & 31, hh = lane >> 5;
+    const int T = p.total, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int q8 = T >> 3, r8 = T & 7;
+    const int jb = xcd * q8 + min(xcd, r8), je = jb + q8 + (xcd < r8 ? 1 : 0);
+    const int G = ((int)gridDim.x - xcd + 7) >> 3;
+    const int ntiles = p.n / kSN;
+    const int j0 = jb + loc;
+    if (j0 >= je) return;
+    const int ntile_w = (je - j0 + G - 1) / G;
+    const int nsteps = ntile_w * KS;
+
+    // DMA of global step gs into stage st: W pieces wave + 8h (16 x 16 rows), A pieces wave + 8h
+    // (16 x 16 rows); lane -> (row 16i + lane / 4, LDS unit lane % 4 <- global unit
+    // (lane % 4) ^ ((row >> 2) & 3))
+    auto issue = [&](int gs, int st) {
+        const int jt = j0 + G * (gs / KS), ks = gs % KS;
+        const int mt = jt / ntiles, m0 = mt * kSM_, n0 = (jt - mt * ntiles) * kSN;
+        char* const sb = smem + st * kSStage;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = wave + 8 * h, row = 16 * i + (lane >> 2);
+            const int gc = ks * (kSK / 8) + ((lane & 3) ^ ((row >> 2) & 3));
+            const int wr = min(n0 + row, p.n - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(p.w + (size_t)wr * p.k + gc * 8),
+                                             (__attribute__((address_space(3))) void*)(sb + i * 1024), 16, 0, 0);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int i = wave + 8 * h, row = 16 * i + (lane >> 2);
+            const int gc = ks * (kSK / 8) + ((lane & 3) ^ ((row >> 2) & 3));
+            const int ar = min(m0 + row, p.m - 1);
+            __builtin_amdgcn_global_load_lds((const void*)a_src<GATHER>(p, ar, gc),
+                                             (__attribute__((address_space(3))) void*)(sb + kSN * 64 + i * 1024), 16,
+                                             0, 0);
+        }
+    };
+    issue(0, 0);
+    if (nsteps > 1) issue(1, 1);
+    if (nsteps > 2) issue(2, 2);
+
+    unsigned wro[4], aro[2];
+    int wsw[4], asw[2];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int wrow = wn * 128 + 32 * b + r;
+        wro[b] = (unsigned)(wrow * 64), wsw[b] = (wrow >> 2) & 3;
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int arow = wm * 64 + 32 * b + r;
+        aro[b] = (unsigned)(kSN * 64 + arow * 64), asw[b] = (arow >> 2) & 3;
+    }
+    int st = 0;
+    for (int t = 0; t < ntile_w; ++t) {
+        const int jt = j0 + G * t;
+        const int mt = jt / ntiles, m0 = mt * kSM_, n0 = (jt - mt * ntiles) * kSN;
+        f32x16 acc[4][2] = {};  // [n block][m block]
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int gs = t * KS + ks;
+            // step gs landed (steps gs + 1, gs + 2 stay in flight: 4 DMAs each per wave), then
+            // everyone's; past this barrier every wave is done with step gs − 1's stage
+            if (gs + 2 < nsteps) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+            else if (gs + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (gs + 3 < nsteps) issue(gs + 3, st == 0 ? 3 : st - 1);
+            const unsigned sb = (unsigned)(st * kSStage);
+            st = (st + 1) & 3;
+#pragma unroll
+            for (int s = 0; s < kSK / 16; ++s) {
+                const int u = 2 * s + hh;
+                f16x8 wf[4], af[2];
+#pragma unroll
+                for (int b = 0; b < 4; ++b) wf[b] = *(lds_f16x8*)(lds + sb + wro[b] + ((u ^ wsw[b]) << 4));
+#pragma unroll
+                for (int b = 0; b < 2; ++b) af[b] = *(lds_f16x8*)(lds + sb + aro[b] + ((u ^ asw[b]) << 4));
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+                    for (int mb = 0; mb < 2; ++mb)
+                        acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[nb], af[mb], acc[nb][mb], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const int row = m0 + wm * 64 + 32 * mb + r;
+            if (row >= p.m) continue;
+#pragma unroll
+            for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    epi_store<EPI>(p, row, n0 + wn * 128 + 32 * nb + 8 * g + 4 * hh, acc[nb][mb], g);
+        }
+    }
+}
+
 // The wide form where it fills the chip: at least one round of its 256 x 128 tiles (n a multiple of
 // 128). lg_linear_set_wide(0 / 1) or LG_LINEAR_WIDE=0 / 1 forces it off / on (where n allows), for
 // tests and A/B timing; -1 (the default) chooses by size.
@@ -376,7 +525,7 @@ int wide_mode() {
     if (v == -2) {
         const char* e = std::getenv("LG_LINEAR_WIDE");
         int expect = -2;
-        g_wide.compare_exchange_strong(expect, e ? (e[0] == '1' ? 1 : 0) : -1);
+        g_wide.compare_exchange_strong(expect, e ? (e[0] == '2' ? 2 : e[0] == '1' ? 1 : 0) : -1);
         v = g_wide.load();
     }
     return v;
@@ -384,12 +533,34 @@ int wide_mode() {
 bool use_wide(const LinArgs& p) {
     if (p.n % kWN) return false;
     const int w = wide_mode();
-    if (w >= 0) return w == 1;
+    if (w >= 0) return w >= 1;
     return (long)((p.m + kWM - 1) / kWM) * (p.n / kWN) >= 256;
+}
+// the square form: forced (mode 2), or by size where its tiles fill whole rounds of the chip
+// (N = 512 at P = 16, N = 1024: cat 36.5 -> 33.2 us, cross qk|v 27.5 -> 25.1; N = 256 / 768 take
+// half / one and a half rounds of it and stay on the 256 x 128 form; linear_ab_square.jsonl)
+bool use_sq(const LinArgs& p) {
+    if (p.n % kSN) return false;
+    const int w = wide_mode();
+    if (w >= 0) return w == 2;
+    const long t = (long)((p.m + kSM_ - 1) / kSM_) * (p.n / kSN);
+    return t >= kWGrid && (t % kWGrid == 0 || t >= 4 * kWGrid);
 }
 
 template <int EPI, bool GATHER>
 int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
+    if (use_sq(p)) {
+        p.mtiles = (p.m + kSM_ - 1) / kSM_;
+        p.total = p.mtiles * (p.n / kSN);
+        const int grid = p.total < kWGrid ? p.total : kWGrid;
+        if (p.k == 256)
+            hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 8>), dim3(grid), dim3(512), 0, stream, p);
+        else
+            hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 16>), dim3(grid), dim3(512), 0, stream, p);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
+                               : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, what, hipGetErrorString(e));
+    }
     if (use_wide(p)) {
         p.mtiles = (p.m + kWM - 1) / kWM;
         p.total = p.mtiles * (p.n / kWN);
@@ -484,7 +655,7 @@ int32_t lg_linear_split2(const void* x, const void* w, const void* bias, int32_t
 
 int32_t lg_linear_set_wide(int32_t mode) {
     wide_mode();
-    return g_wide.exchange(mode < 0 ? -1 : (mode ? 1 : 0));
+    return g_wide.exchange(mode < 0 ? -1 : (mode > 2 ? 2 : mode));
 }
 
 }  // extern "C"

@@ -488,7 +488,8 @@ def test_torch_glue_runs_pairs_one_by_one():
 @pytest.mark.gpu
 @pytest.mark.parametrize("pairs,n0,n1", [(3, 37, 70), (2, 1000, 777), (16, 1024, 1024)])
 def test_wide_projections_equal_narrow(pairs, n0, n1):
-    """The projections' 256 x 128-tile form (csrc/lightglue_linear.hip linear_wide_kernel, taken for
+    """The projections' 256 x 128-tile and 256 x 256-tile forms (csrc/lightglue_linear.hip linear_wide_kernel /
+    linear_sq_kernel, taken for
     launches of at least one round of its tiles: several image pairs per forward) gives the bits of
     the 64 x 64 form on every fused entry point — ragged row counts (rows past m in a tile), both
     K (256 and 512), residual on and off, the A-gather of lg_linear_cat, the per-image scatters."""
@@ -529,9 +530,11 @@ def test_wide_projections_equal_narrow(pairs, n0, n1):
             narrow = [flat(o) for o in run()]
             lib.lg_linear_set_wide(1)
             wide = [flat(o) for o in run()]
+            lib.lg_linear_set_wide(2)  # 256 x 256 tiles, 32-deep K steps
+            square = [flat(o) for o in run()]
             torch.cuda.synchronize()
         finally:
             lib.lg_linear_set_wide(prev)
-        for a, b in zip(narrow, wide):
-            for ta, tb in zip(a, b):
-                assert torch.equal(ta, tb)
+        for a, b, c in zip(narrow, wide, square):
+            for ta, tb, tc in zip(a, b, c):
+                assert torch.equal(ta, tb) and torch.equal(ta, tc)

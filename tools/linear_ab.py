@@ -1,5 +1,5 @@
 """Diagnostic: the matcher projections (include/lightglue_glue.h lg_linear*) in their 64 x 64 and
-256 x 128-tile forms (lg_linear_set_wide 0 / 1) at P image pairs of n keypoints per image, graph
+256 x 128-tile and 256 x 256-tile forms (lg_linear_set_wide 0 / 1 / 2) at P image pairs of n keypoints per image, graph
 replay of back-to-back launches, interleaved; TFLOP/s of each.
 
     python tools/linear_ab.py [P] [n]"""
@@ -42,7 +42,7 @@ def main():
     K = 20
     graphs = {}
     for name, (fn, _) in ops.items():
-        for wide in (0, 1):
+        for wide in (0, 1, 2):
             lib.lg_linear_set_wide(wide)
             with torch.cuda.stream(st):
                 fn()
@@ -65,9 +65,9 @@ def main():
             times[k].append(e0.elapsed_time(e1) * 1e3 / K)
     for name, (_, kn) in ops.items():
         row = {"op": name, "M": M}
-        for wide in (0, 1):
+        for wide in (0, 1, 2):
             us = statistics.median(times[(name, wide)])
-            row["wide" if wide else "narrow"] = {"us": round(us, 2), "tflops": round(2.0 * M * kn / us / 1e6, 1)}
+            row[("narrow", "wide", "square")[wide]] = {"us": round(us, 2), "tflops": round(2.0 * M * kn / us / 1e6, 1)}
         print(json.dumps(row), flush=True)
 
 
