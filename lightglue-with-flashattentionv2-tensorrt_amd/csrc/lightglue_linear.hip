@@ -246,6 +246,71 @@ __device__ __forceinline__ void epi_store(const LinArgs& p, int row, int n, cons
     }
 }
 
+// ---- per-tile DMA sources of the 256-row forms: each wave's W and A pieces of a tile, computed once
+// per tile (row clamps, the swizzled unit, the A-gather's image and head-major offset) so that a K
+// step's DMA is one address add per piece. BK-deep steps: a 1-KiB piece is 1024 / (2 BK) rows; lane
+// -> (row RP i + lane / U, LDS unit lane % U <- global unit (lane % U) ^ swz(row)), U = BK / 8 units a row
+template <int NWP, int NAP>
+struct TileSrc {
+    const f16* w[NWP];
+    const f16* a[NAP];  // A rows (the gather: x rows)
+    const f16* c[NAP];  // the gather: head 0 of the row in its image's [pairs, heads, ni, 64] tensor
+    int hs[NAP];        // the gather: elements between heads there (ni * 64)
+};
+template <int BK>
+__device__ __forceinline__ int src_unit(int row, int pos) {
+    return BK == 64 ? (pos ^ ((row >> 1) & 7)) : (pos ^ ((row >> 2) & 3));
+}
+template <bool GATHER, int BK, int NWP, int NAP>
+__device__ __forceinline__ TileSrc<NWP, NAP> tile_src(const LinArgs& p, int m0, int n0, int wave, int lane) {
+    constexpr int U = BK / 8, RP = 1024 / (2 * BK);
+    TileSrc<NWP, NAP> t;
+#pragma unroll
+    for (int h = 0; h < NWP; ++h) {
+        const int row = RP * (wave + 8 * h) + lane / U;
+        const int wr = min(n0 + row, p.n - 1);
+        t.w[h] = p.w + (size_t)wr * p.k + src_unit<BK>(row, lane % U) * 8;
+    }
+#pragma unroll
+    for (int h = 0; h < NAP; ++h) {
+        const int row = RP * (wave + 8 * h) + lane / U;
+        const int ar = min(m0 + row, p.m - 1);
+        const int gu8 = src_unit<BK>(row, lane % U) * 8;
+        if constexpr (!GATHER) {
+            t.a[h] = p.a + (size_t)ar * p.k + gu8;
+        } else {
+            t.a[h] = p.a + (size_t)ar * (p.k / 2) + gu8;
+            const LinRow lr = lin_row(p, ar, 0);
+            t.c[h] = (lr.first ? p.ctx0 : p.ctx1) + lr.off + gu8;
+            t.hs[h] = (lr.first ? p.n0 : p.n1) * kD;
+        }
+    }
+    return t;
+}
+// K step ks (compile-time after unrolling; K = KS BK) of a tile into the stage at sb: W pieces
+// wave + 8h at sb, A pieces at sb + BN BK 2
+template <bool GATHER, int BK, int KS, int BN, int NWP, int NAP>
+__device__ __forceinline__ void tile_issue(const TileSrc<NWP, NAP>& t, int ks, char* sb, int wave) {
+#pragma unroll
+    for (int h = 0; h < NWP; ++h)
+        __builtin_amdgcn_global_load_lds((const void*)(t.w[h] + ks * BK),
+                                         (__attribute__((address_space(3))) void*)(sb + (wave + 8 * h) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int h = 0; h < NAP; ++h) {
+        const f16* src;
+        if constexpr (!GATHER) {
+            src = t.a[h] + ks * BK;
+        } else {
+            constexpr int half = KS * BK / 2;
+            const int col = ks * BK;
+            src = col < half ? t.a[h] + col : t.c[h] + ((col - half) / kD) * t.hs[h] + (col - half) % kD;
+        }
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(sb + BN * BK * 2 + (wave + 8 * h) * 1024),
+                                         16, 0, 0);
+    }
+}
+
 // ---- the wide form, for launches with many rows (several image pairs per forward) ----
 // Workgroup: 256 rows (m) x 128 output channels (n) a tile, persistent over tiles (the DMA ring
 // runs on across tile seams: the next tile's first two K steps load during the current tile's
@@ -282,33 +347,14 @@ __global__ __launch_bounds__(512, 1) void linear_wide_kernel(LinArgs p) {
     const int ntile_w = (je - j0 + G - 1) / G;  // tiles of this workgroup
     const int nsteps = ntile_w * KS;            // K steps over all of them
 
-    // DMA of global step gs (tile gs / KS, K step gs % KS) into stage st: W pieces wave, wave + 8
-    // (16 x 8 rows), A pieces wave + 8i (32 x 8 rows); lane -> (row 8i + lane / 8, LDS unit
-    // lane % 8 <- global unit (lane % 8) ^ ((row >> 1) & 7))
-    auto issue = [&](int gs, int st) {
-        const int jt = j0 + G * (gs / KS), ks = gs % KS;
-        const int mt = jt / ntiles, m0 = mt * kWM, n0 = (jt - mt * ntiles) * kWN;
-        char* const sb = smem + st * kWStage;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int i = wave + 8 * h, row = 8 * i + (lane >> 3);
-            const int gc = ks * (kWK / 8) + ((lane & 7) ^ ((row >> 1) & 7));
-            const int wr = min(n0 + row, p.n - 1);
-            __builtin_amdgcn_global_load_lds((const void*)(p.w + (size_t)wr * p.k + gc * 8),
-                                             (__attribute__((address_space(3))) void*)(sb + i * 1024), 16, 0, 0);
-        }
-#pragma unroll
-        for (int h = 0; h < 4; ++h) {
-            const int i = wave + 8 * h, row = 8 * i + (lane >> 3);
-            const int gc = ks * (kWK / 8) + ((lane & 7) ^ ((row >> 1) & 7));
-            const int ar = min(m0 + row, p.m - 1);
-            __builtin_amdgcn_global_load_lds((const void*)a_src<GATHER>(p, ar, gc),
-                                             (__attribute__((address_space(3))) void*)(sb + kWN * 128 + i * 1024), 16,
-                                             0, 0);
-        }
+    // DMA sources of this workgroup's tile t (computed once per tile)
+    auto src_of = [&](int t) {
+        const int jt = j0 + G * t, mt = jt / ntiles;
+        return tile_src<GATHER, kWK, 2, 4>(p, mt * kWM, (jt - mt * ntiles) * kWN, wave, lane);
     };
-    issue(0, 0);
-    if (nsteps > 1) issue(1, 1);
+    TileSrc<2, 4> cur = src_of(0), nxt = cur;
+    tile_issue<GATHER, kWK, KS, kWN>(cur, 0, smem, wave);
+    tile_issue<GATHER, kWK, KS, kWN>(cur, 1, smem + kWStage, wave);
 
     unsigned wro[2], aro[2];  // per block: row offset and swizzle key of this lane's fragment row
     int wsw[2], asw[2];
@@ -322,6 +368,8 @@ __global__ __launch_bounds__(512, 1) void linear_wide_kernel(LinArgs p) {
     for (int t = 0; t < ntile_w; ++t) {
         const int jt = j0 + G * t;
         const int mt = jt / ntiles, m0 = mt * kWM, n0 = (jt - mt * ntiles) * kWN;
+        const bool more = t + 1 < ntile_w;
+        if (more) nxt = src_of(t + 1);
         f32x16 acc[2][2] = {};  // [n block][m block]
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -332,7 +380,11 @@ __global__ __launch_bounds__(512, 1) void linear_wide_kernel(LinArgs p) {
             if (gs + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
-            if (gs + 2 < nsteps) issue(gs + 2, st == 0 ? 2 : st - 1);
+            {
+                char* const fb = smem + (st == 0 ? 2 : st - 1) * kWStage;
+                if (ks + 2 < KS) tile_issue<GATHER, kWK, KS, kWN>(cur, ks + 2, fb, wave);
+                else if (more) tile_issue<GATHER, kWK, KS, kWN>(nxt, ks + 2 - KS, fb, wave);
+            }
             const unsigned sb = (unsigned)(st * kWStage);
             st = st == 2 ? 0 : st + 1;
 #pragma unroll
@@ -361,45 +413,12 @@ __global__ __launch_bounds__(512, 1) void linear_wide_kernel(LinArgs p) {
             const int row = m0 + wm * 64 + 32 * mb + r;
             if (row >= p.m) continue;
 #pragma unroll
-            for (int nb = 0; nb < 2; ++nb) {
+            for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int n = n0 + wn * 64 + 32 * nb + 8 * g + 4 * hh;
-                    const f16x4 b4 = *reinterpret_cast<const f16x4*>(p.bias + n);
-                    float v[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) v[u] = acc[nb][mb][4 * g + u] + (float)b4[u];
-                    if constexpr (EPI == EPI_BIAS) {
-                        if (p.res) {
-                            const f16x4 rr = *reinterpret_cast<const f16x4*>(p.res + (size_t)row * p.n + n);
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) v[u] += (float)rr[u];
-                        }
-                        *reinterpret_cast<f16x4*>(p.out[0] + (size_t)row * p.n + n) =
-                            f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
-                    } else {
-                        const int hd = p.heads * kD;
-                        const int part = n / hd, h = (n % hd) / kD, d = n % kD;
-                        const LinRow lr = lin_row(p, row, h);
-                        if constexpr (EPI == EPI_QKV_ROTARY) {
-                            if (part < 2) {
-                                const f16x4 cc = *reinterpret_cast<const f16x4*>(p.cosv + (size_t)row * kD + d);
-                                const f16x4 ss = *reinterpret_cast<const f16x4*>(p.sinv + (size_t)row * kD + d);
-#pragma unroll
-                                for (int u = 0; u < 4; u += 2) {
-                                    const float x0 = v[u], x1 = v[u + 1];
-                                    v[u] = x0 * (float)cc[u] - x1 * (float)ss[u];
-                                    v[u + 1] = x1 * (float)cc[u + 1] + x0 * (float)ss[u + 1];
-                                }
-                            }
-                        }
-                        f16* dst = p.out[(lr.first ? 0 : (EPI == EPI_QKV_ROTARY ? 3 : 1)) +
-                                         (EPI == EPI_QKV_ROTARY ? part : 2 * part)];
-                        *reinterpret_cast<f16x4*>(dst + lr.off + d) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
-                    }
-                }
-            }
+                for (int g = 0; g < 4; ++g)
+                    epi_store<EPI>(p, row, n0 + wn * 64 + 32 * nb + 8 * g + 4 * hh, acc[nb][mb], g);
         }
+        cur = nxt;
     }
 }
 
@@ -410,11 +429,11 @@ __global__ __launch_bounds__(512, 1) void linear_wide_kernel(LinArgs p) {
 // the other forms: same bits. (lg_linear_set_wide(2) / LG_LINEAR_WIDE=2, where n % 256 == 0.)
 constexpr int kSM_ = 256, kSN = 256, kSK = 32;
 constexpr int kSStage = (kSM_ + kSN) * kSK * 2;  // 32 KiB
-constexpr int kSStages = 4;
 
-template <int EPI, bool GATHER, int KS>
+// NST stages (4: 128 KiB; 5: the whole 160 KiB), NST − 1 steps in flight
+template <int EPI, bool GATHER, int KS, int NST>
 __global__ __launch_bounds__(512, 1) void linear_sq_kernel(LinArgs p) {
-    __shared__ __attribute__((aligned(16))) char smem[kSStages * kSStage];  // 128 KiB
+    __shared__ __attribute__((aligned(16))) char smem[NST * kSStage];
     lds_char* const lds = (lds_char*)smem;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -430,34 +449,14 @@ __global__ __launch_bounds__(512, 1) void linear_sq_kernel(LinArgs p) {
     const int ntile_w = (je - j0 + G - 1) / G;
     const int nsteps = ntile_w * KS;
 
-    // DMA of global step gs into stage st: W pieces wave + 8h (16 x 16 rows), A pieces wave + 8h
-    // (16 x 16 rows); lane -> (row 16i + lane / 4, LDS unit lane % 4 <- global unit
-    // (lane % 4) ^ ((row >> 2) & 3))
-    auto issue = [&](int gs, int st) {
-        const int jt = j0 + G * (gs / KS), ks = gs % KS;
-        const int mt = jt / ntiles, m0 = mt * kSM_, n0 = (jt - mt * ntiles) * kSN;
-        char* const sb = smem + st * kSStage;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int i = wave + 8 * h, row = 16 * i + (lane >> 2);
-            const int gc = ks * (kSK / 8) + ((lane & 3) ^ ((row >> 2) & 3));
-            const int wr = min(n0 + row, p.n - 1);
-            __builtin_amdgcn_global_load_lds((const void*)(p.w + (size_t)wr * p.k + gc * 8),
-                                             (__attribute__((address_space(3))) void*)(sb + i * 1024), 16, 0, 0);
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int i = wave + 8 * h, row = 16 * i + (lane >> 2);
-            const int gc = ks * (kSK / 8) + ((lane & 3) ^ ((row >> 2) & 3));
-            const int ar = min(m0 + row, p.m - 1);
-            __builtin_amdgcn_global_load_lds((const void*)a_src<GATHER>(p, ar, gc),
-                                             (__attribute__((address_space(3))) void*)(sb + kSN * 64 + i * 1024), 16,
-                                             0, 0);
-        }
+    // DMA sources of this workgroup's tile t (computed once per tile)
+    auto src_of = [&](int t) {
+        const int jt = j0 + G * t, mt = jt / ntiles;
+        return tile_src<GATHER, kSK, 2, 2>(p, mt * kSM_, (jt - mt * ntiles) * kSN, wave, lane);
     };
-    issue(0, 0);
-    if (nsteps > 1) issue(1, 1);
-    if (nsteps > 2) issue(2, 2);
+    TileSrc<2, 2> cur = src_of(0), nxt = cur;
+#pragma unroll
+    for (int i = 0; i < NST - 1; ++i) tile_issue<GATHER, kSK, KS, kSN>(cur, i, smem + i * kSStage, wave);
 
     unsigned wro[4], aro[2];
     int wsw[4], asw[2];
@@ -475,19 +474,27 @@ __global__ __launch_bounds__(512, 1) void linear_sq_kernel(LinArgs p) {
     for (int t = 0; t < ntile_w; ++t) {
         const int jt = j0 + G * t;
         const int mt = jt / ntiles, m0 = mt * kSM_, n0 = (jt - mt * ntiles) * kSN;
+        const bool more = t + 1 < ntile_w;
+        if (more) nxt = src_of(t + 1);
         f32x16 acc[4][2] = {};  // [n block][m block]
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const int gs = t * KS + ks;
-            // step gs landed (steps gs + 1, gs + 2 stay in flight: 4 DMAs each per wave), then
-            // everyone's; past this barrier every wave is done with step gs − 1's stage
-            if (gs + 2 < nsteps) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-            else if (gs + 1 < nsteps) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+            // step gs landed (up to NST − 2 later steps stay in flight: 4 DMAs each per wave),
+            // then everyone's; past this barrier every wave is done with step gs − 1's stage
+            const int later = min(NST - 2, nsteps - 1 - gs);
+            if (later >= 3) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+            else if (later == 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+            else if (later == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
-            if (gs + 3 < nsteps) issue(gs + 3, st == 0 ? 3 : st - 1);
+            {
+                char* const fb = smem + (st == 0 ? NST - 1 : st - 1) * kSStage;
+                if (ks + NST - 1 < KS) tile_issue<GATHER, kSK, KS, kSN>(cur, ks + NST - 1, fb, wave);
+                else if (more) tile_issue<GATHER, kSK, KS, kSN>(nxt, ks + NST - 1 - KS, fb, wave);
+            }
             const unsigned sb = (unsigned)(st * kSStage);
-            st = (st + 1) & 3;
+            st = st == NST - 1 ? 0 : st + 1;
 #pragma unroll
             for (int s = 0; s < kSK / 16; ++s) {
                 const int u = 2 * s + hh;
@@ -513,6 +520,7 @@ __global__ __launch_bounds__(512, 1) void linear_sq_kernel(LinArgs p) {
                 for (int g = 0; g < 4; ++g)
                     epi_store<EPI>(p, row, n0 + wn * 128 + 32 * nb + 8 * g + 4 * hh, acc[nb][mb], g);
         }
+        cur = nxt;
     }
 }
 
@@ -542,7 +550,7 @@ bool use_wide(const LinArgs& p) {
 bool use_sq(const LinArgs& p) {
     if (p.n % kSN) return false;
     const int w = wide_mode();
-    if (w >= 0) return w == 2;
+    if (w >= 0) return w >= 2;
     const long t = (long)((p.m + kSM_ - 1) / kSM_) * (p.n / kSN);
     return t >= kWGrid && (t % kWGrid == 0 || t >= 4 * kWGrid);
 }
@@ -553,10 +561,16 @@ int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
         p.mtiles = (p.m + kSM_ - 1) / kSM_;
         p.total = p.mtiles * (p.n / kSN);
         const int grid = p.total < kWGrid ? p.total : kWGrid;
-        if (p.k == 256)
-            hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 8>), dim3(grid), dim3(512), 0, stream, p);
-        else
-            hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 16>), dim3(grid), dim3(512), 0, stream, p);
+        if (wide_mode() == 3) {  // (A/B: five stages)
+            if (p.k == 256)
+                hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 8, 5>), dim3(grid), dim3(512), 0, stream, p);
+            else
+                hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 16, 5>), dim3(grid), dim3(512), 0, stream, p);
+        } else if (p.k == 256) {
+            hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 8, 4>), dim3(grid), dim3(512), 0, stream, p);
+        } else {
+            hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 16, 4>), dim3(grid), dim3(512), 0, stream, p);
+        }
         const hipError_t e = hipGetLastError();
         return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                                : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, what, hipGetErrorString(e));
@@ -655,7 +669,7 @@ int32_t lg_linear_split2(const void* x, const void* w, const void* bias, int32_t
 
 int32_t lg_linear_set_wide(int32_t mode) {
     wide_mode();
-    return g_wide.exchange(mode < 0 ? -1 : (mode > 2 ? 2 : mode));
+    return g_wide.exchange(mode < 0 ? -1 : (mode > 3 ? 3 : mode));
 }
 
 }  // extern "C"

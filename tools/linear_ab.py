@@ -2,7 +2,7 @@
 256 x 128-tile and 256 x 256-tile forms (lg_linear_set_wide 0 / 1 / 2) at P image pairs of n keypoints per image, graph
 replay of back-to-back launches, interleaved; TFLOP/s of each.
 
-    python tools/linear_ab.py [P] [n]"""
+    python tools/linear_ab.py [P] [n] [op substring] [modes, e.g. 012]"""
 import json
 import os
 import statistics
@@ -19,6 +19,8 @@ from lightglue_amd import matcher as mt  # noqa: E402
 def main():
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 16
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    only = sys.argv[3] if len(sys.argv) > 3 else ""  # op-name substring (counter runs)
+    modes = tuple(int(c) for c in sys.argv[4]) if len(sys.argv) > 4 else (0, 1, 2)
     lib = _lib.load()
     dev, dt, h = torch.device("cuda:0"), torch.float16, 4
     M = P * 2 * n
@@ -41,8 +43,9 @@ def main():
     st = torch.cuda.Stream(dev)
     K = 20
     graphs = {}
+    ops = {k: v for k, v in ops.items() if only in k}
     for name, (fn, _) in ops.items():
-        for wide in (0, 1, 2):
+        for wide in modes:
             lib.lg_linear_set_wide(wide)
             with torch.cuda.stream(st):
                 fn()
@@ -65,9 +68,9 @@ def main():
             times[k].append(e0.elapsed_time(e1) * 1e3 / K)
     for name, (_, kn) in ops.items():
         row = {"op": name, "M": M}
-        for wide in (0, 1, 2):
+        for wide in modes:
             us = statistics.median(times[(name, wide)])
-            row[("narrow", "wide", "square")[wide]] = {"us": round(us, 2), "tflops": round(2.0 * M * kn / us / 1e6, 1)}
+            row[("narrow", "wide", "square", "square5")[wide]] = {"us": round(us, 2), "tflops": round(2.0 * M * kn / us / 1e6, 1)}
         print(json.dumps(row), flush=True)
 
 
