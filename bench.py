@@ -671,7 +671,7 @@ def matcher_e2e(torch, device, stream, rank, sizes=(512, 1024, 2048), reps=10):
     return res
 
 
-def matcher_batched_pairs(torch, device, stream, rank, n=1024, pairs=(1, 4, 8, 16), reps=10, streams=2):
+def matcher_batched_pairs(torch, device, stream, rank, n=1024, pairs=(1, 4, 8, 16, 32), reps=10, streams=2):
     """BASELINE configs[4] on one GPU: P image pairs stacked in the batch dimension of ONE forward
     (every projection and glue kernel runs once on all P pairs' rows; each layer's self and cross
     attention is one grouped launch of P-batch calls), fp16, N0 = N1 = n; one captured forward
@@ -1050,15 +1050,16 @@ def main():
             "tflops": round(B * flops / (tb * 1e-3) / 1e12, 2),
             "frac": round(B * flops / (tb * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4),
         }
-        # more calls per launch (a pair stream of 16 / 32 pairs' calls stacked): the planner's plan,
+        # more calls per launch (a pair stream of 16 / 32 / 64 pairs' calls stacked): the planner's plan,
         # graph replay of 50 back-to-back launches
         sweep_b = {}
-        for B2 in (16, 32):
+        for B2 in (16, 32, 64):
             qs, ks, vs = (torch.from_numpy(x).to(device).half().contiguous()
                           for x in synth.qkv(310 + B2 + rank, nq, nkv, batch=B2))
             os_ = torch.empty_like(qs)
-            # the opt-in persistent streaming kernel (forced plan 23; mha_hd64_set_stream_mode(1)),
-            # timed interleaved with the planner's plan (A/B/A/B replays: no order or clock-drift bias)
+            # the persistent streaming kernel forced (plan 23; the planner's own choice past one round
+            # of 128-row blocks), timed interleaved with the planner's plan (A/B/A/B replays: no order
+            # or clock-drift bias)
             def stream_launch(qs=qs, ks=ks, vs=vs, os_=os_, B2=B2):
                 st = lib.mha_hd64_launch_forced(qs.data_ptr(), ks.data_ptr(), vs.data_ptr(), os_.data_ptr(), B2, 4, nq,
                                                 nkv, 0, 0, 23, 0, 0, ws_buf2.data_ptr(), ws_buf2.numel(),
@@ -1089,7 +1090,7 @@ def main():
         # 256-workgroup kernels) against an ideal 0.43 us of MFMA work.
         result["roofline"]["ideal_us_at_peak"] = round(flops / (PEAK_F16_TFLOPS * 1e12) * 1e6, 4)
         result["roofline"]["launch_boundary_floor_us"] = 1.45
-        result["roofline"]["saturated"] = {"form": f"{best_b} calls per launch (batched), best of 8 / 16 / 32",
+        result["roofline"]["saturated"] = {"form": f"{best_b} calls per launch (batched), best of 8 / 16 / 32 / 64",
                                            "frac": best, "frac_8_calls": result["batched"]["frac"]}
         # What this instruction mix sustains on the part (measured, not the 2.5 PF spec): the
         # head_dim-64 step's MFMAs with its softmax density beside them, registers only
