@@ -60,6 +60,7 @@ struct LinArgs {
     int m, n, k;
     int heads, n0, n1; // per-image split: m = pairs x (n0 + n1) rows, pair-major (n0 of image 0, n1 of image 1)
     int mtiles, total;
+    int st16;          // 256-row forms, EPI_BIAS: 16-B row-segment stores (LG_LINEAR_ST16=1; A/B)
 };
 
 // Row `row` of the stacked rows -> its image and the offset of its head-h segment in that image's
@@ -246,6 +247,48 @@ __device__ __forceinline__ void epi_store(const LinArgs& p, int row, int n, cons
     }
 }
 
+// One 32 x 32 block of a 256-row form (lane = activation row `row`, channels nb0 + 8g + 4hh + t in
+// acc[4g + t]): with p.st16 and EPI_BIAS, v_permlane32_swap pairs (g, g + 1) between the two
+// half-waves so each lane stores 8 consecutive channels (16 B) per pair; else epi_store per group.
+template <int EPI>
+__device__ __forceinline__ void epi_block(const LinArgs& p, int row, int nb0, const f32x16& acc, int hh) {
+    if constexpr (EPI == EPI_BIAS) {
+        if (p.st16) {
+            typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+            typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+            u32x2_ rk[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int n = nb0 + 8 * g + 4 * hh;
+                const f16x4 b4 = *reinterpret_cast<const f16x4*>(p.bias + n);
+                float v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = acc[4 * g + u] + (float)b4[u];
+                if (p.res) {
+                    const f16x4 rr = *reinterpret_cast<const f16x4*>(p.res + (size_t)row * p.n + n);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) v[u] += (float)rr[u];
+                }
+                rk[g] = __builtin_bit_cast(u32x2_, f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]});
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k += 2) {
+#pragma unroll
+                for (int w = 0; w < 2; ++w) {
+                    const auto sw = __builtin_amdgcn_permlane32_swap(rk[k][w], rk[k + 1][w], false, false);
+                    rk[k][w] = sw[0];
+                    rk[k + 1][w] = sw[1];
+                }
+                *reinterpret_cast<u32x4_*>(p.out[0] + (size_t)row * p.n + nb0 + 8 * (k + hh)) =
+                    u32x4_{rk[k][0], rk[k][1], rk[k + 1][0], rk[k + 1][1]};
+            }
+            return;
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) epi_store<EPI>(p, row, nb0 + 8 * g + 4 * hh, acc, g);
+}
+
 // ---- per-tile DMA sources of the 256-row forms: each wave's W and A pieces of a tile, computed once
 // per tile (row clamps, the swizzled unit, the A-gather's image and head-major offset) so that a K
 // step's DMA is one address add per piece. BK-deep steps: a 1-KiB piece is 1024 / (2 BK) rows; lane
@@ -413,10 +456,7 @@ __global__ __launch_bounds__(512, 1) void linear_wide_kernel(LinArgs p) {
             const int row = m0 + wm * 64 + 32 * mb + r;
             if (row >= p.m) continue;
 #pragma unroll
-            for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    epi_store<EPI>(p, row, n0 + wn * 64 + 32 * nb + 8 * g + 4 * hh, acc[nb][mb], g);
+            for (int nb = 0; nb < 2; ++nb) epi_block<EPI>(p, row, n0 + wn * 64 + 32 * nb, acc[nb][mb], hh);
         }
         cur = nxt;
     }
@@ -515,10 +555,7 @@ __global__ __launch_bounds__(512, 1) void linear_sq_kernel(LinArgs p) {
             const int row = m0 + wm * 64 + 32 * mb + r;
             if (row >= p.m) continue;
 #pragma unroll
-            for (int nb = 0; nb < 4; ++nb)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    epi_store<EPI>(p, row, n0 + wn * 128 + 32 * nb + 8 * g + 4 * hh, acc[nb][mb], g);
+            for (int nb = 0; nb < 4; ++nb) epi_block<EPI>(p, row, n0 + wn * 128 + 32 * nb, acc[nb][mb], hh);
         }
         cur = nxt;
     }
@@ -555,8 +592,17 @@ bool use_sq(const LinArgs& p) {
     return t >= kWGrid && (t % kWGrid == 0 || t >= 4 * kWGrid);
 }
 
+int st16_env() {
+    static const int v = [] {
+        const char* e = std::getenv("LG_LINEAR_ST16");
+        return (e && e[0] == '1') ? 1 : 0;
+    }();
+    return v;
+}
+
 template <int EPI, bool GATHER>
 int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
+    p.st16 = st16_env();
     if (use_sq(p)) {
         p.mtiles = (p.m + kSM_ - 1) / kSM_;
         p.total = p.mtiles * (p.n / kSN);
