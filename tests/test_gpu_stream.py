@@ -325,3 +325,46 @@ def test_stream_kernel_bitwise_repeatable(waves, batch, dev):
         _launch(lib, q, k, v, o, ws=ws, waves=waves)
         torch.cuda.synchronize()
         assert torch.equal(o, first)
+
+
+# ---- the reference's golden fixtures through plan 23 ----
+from conftest import golden_cases, load_golden  # noqa: E402
+
+
+def _fixture_batch(nq, waves):
+    """Copies of a fixture stacked in the batch so that every workgroup of the forced form walks at
+    least two items (grid = min(items, 512 / 256 workgroups for 4 / 8 waves))."""
+    items = 4 * -(-nq // (32 * waves))
+    cap = 512 if waves == 4 else 256
+    return -(-(2 * cap + cap // 4) // items)
+
+
+@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("name", golden_cases())
+def test_stream_kernel_matches_reference_fixtures(name, waves, dev):
+    """Every golden fixture (outputs of the reference's PyTorch Attention) through the streaming
+    kernel, both forms, both output types, under the single-call kernels' regression guards
+    (test_gpu_parity.py: fp16 out |d| <= 1.5e-3 s + 2^-11 |ref|, fp32 out 1.5e-3 s); the fixture is
+    copied B times into the batch so items sit at every seam position of the K/V ring, and every
+    copy must give the same bits (an item's result may not depend on its neighbours)."""
+    from test_gpu_parity import REG_F32OUT, _regress16, _scale
+
+    from lightglue_amd import _lib
+
+    lib = _lib.load()
+    g = load_golden(name)
+    nq = g["q"].shape[2]
+    B = _fixture_batch(nq, waves)
+    q16, k16, v16 = (np.ascontiguousarray(np.repeat(g[x], B, axis=0)) for x in ("q", "k", "v"))
+    q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+    for out_dt in (torch.float16, torch.float32):
+        o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
+        _launch(lib, q, k, v, o, waves=waves)
+        torch.cuda.synchronize()
+        assert torch.equal(o, o[:1].expand_as(o)), "batch copies of one fixture differ"
+        got = o[:1].float().cpu().numpy()[:, :, g["rows"]]
+        assert np.isfinite(got).all()
+        if out_dt == torch.float16:
+            _regress16(got, g["o_ref16"], _scale(g))
+        else:
+            assert _maxdiff(got, g["o_ref16"]) <= REG_F32OUT * _scale(g)
