@@ -12,6 +12,11 @@
  * pair-major — pair p's n0 rows of image 0, then its n1 rows of image 1 — so "[n0+n1, ...]"
  * below reads [pairs*(n0+n1), ...], and each per-image head-major tensor "[heads, ni, 64]" reads
  * [pairs, heads, ni, 64] (the batch dimension of the attention calls). pairs = 1: one pair.
+ *
+ * ABI version 2 (round 4): `pairs` inserted after n1 in the split / merge / fused-projection calls
+ * and `batch` in the dual log-softmax and its workspace query. A host built against an older
+ * header links against the same symbol names and would pass shifted arguments: check
+ * lg_glue_abi_version() == LG_GLUE_ABI_VERSION once at load.
  */
 #ifndef LIGHTGLUE_GLUE_H_
 #define LIGHTGLUE_GLUE_H_
@@ -24,6 +29,10 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+#define LG_GLUE_ABI_VERSION 2
+/* The ABI version of the argument lists below that this library implements. */
+int32_t lg_glue_abi_version(void);
 
 /* SelfBlock q/k/v (lightglue.py:111-119, rotary :124-134): qkv [n0+n1, heads*64*3] is the Wqkv
  * output with channel (h*64 + d)*3 + j; cos/sin [n0+n1, 64] the positional encoding (pairs
@@ -90,8 +99,10 @@ int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1
 
 /* Test and benchmark hook: the projections' tile forms for launches of many rows (several image
  * pairs per forward): 0 the 64 x 64 form only, 1 the 256 x 128 form where n allows, 2 the
- * 256 x 256 form where n allows, -1 (the default) chosen by size. Every form gives the same bits.
- * Returns the previous mode. */
+ * 256 x 256 form where n allows, 3 the 256 x 256 form with a fifth ring stage (A/B only), -1 (the
+ * default) chosen by size; values outside -1..3 are clamped. The environment variable
+ * LG_LINEAR_WIDE sets the initial mode the same way. Every form gives the same bits. Returns the
+ * previous mode. */
 int32_t lg_linear_set_wide(int32_t mode);
 
 #ifdef __cplusplus

@@ -41,7 +41,14 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) char lds_char;
 typedef __attribute__((address_space(3))) f16x8 lds_f16x8;
 
-constexpr int kBM = 64, kBN = 64, kKC = 128;  // tile rows, tile channels, K columns per LDS chunk
+// Ablation builds (tools/build_linear_variant.sh -DLG_ABL=bits; diagnostics, never shipped), in the
+// 256-row forms: 1 = no epilogue stores (the accumulators kept live), 2 = no MFMAs (nor their
+// fragment reads), 4 = no operand DMA.
+#ifndef LG_ABL
+#define LG_ABL 0
+#endif
+constexpr int kBM = 64, kBN = 64, kKC = 128;
+// tile rows, tile channels, K columns per LDS chunk
 constexpr int kChunkBytes = 64 * kKC * 2;     // one [64 rows][128 k] fp16 chunk = 16 KiB
 constexpr int kD = 64;                        // head dim
 
@@ -60,7 +67,6 @@ struct LinArgs {
     int m, n, k;
     int heads, n0, n1; // per-image split: m = pairs x (n0 + n1) rows, pair-major (n0 of image 0, n1 of image 1)
     int mtiles, total;
-    int st16;          // 256-row forms, EPI_BIAS: 16-B row-segment stores (default; LG_LINEAR_ST16=0: off)
 };
 
 // Row `row` of the stacked rows -> its image and the offset of its head-h segment in that image's
@@ -89,6 +95,20 @@ __device__ __forceinline__ const f16* a_src(const LinArgs& p, int row, int gc) {
         const LinRow lr = lin_row(p, row, h);
         return (lr.first ? p.ctx0 : p.ctx1) + lr.off + d;
     }
+}
+
+// The projections' output arithmetic, shared by every form (so every form gives the same bits): the
+// GEMM value plus bias is rounded to fp16 once (F.linear's fp16 output, lightglue.py:97-122); the
+// residual add and the rotary (lightglue.py:124-134) then work from that value, as the reference's
+// fp16 model does (x + ffn(...), q * cos + rotate(q) * sin), in fp32 with one rounding each.
+__device__ __forceinline__ f16 lin_val(float acc, f16 b) { return (f16)(acc + (float)b); }
+__device__ __forceinline__ f16 res_add(f16 v, f16 r) { return (f16)((float)v + (float)r); }
+// (x0, x1) of a rotary pair (d, d + 1) -> (x0 c0 - x1 s0, x1 c1 + x0 s1), elements e, e + 1 of v
+template <typename V>
+__device__ __forceinline__ void rot_pair(V& v, int e, f16 c0, f16 s0, f16 c1, f16 s1) {
+    const float x0 = (float)v[e], x1 = (float)v[e + 1];
+    v[e] = (f16)__builtin_fmaf(x0, (float)c0, -(x1 * (float)s0));
+    v[e + 1] = (f16)__builtin_fmaf(x1, (float)c1, x0 * (float)s1);
 }
 
 template <int EPI, bool GATHER, int KC>
@@ -179,15 +199,15 @@ __global__ __launch_bounds__(256) void linear_kernel(LinArgs p) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
         const int n = n0 + wn * 32 + 8 * g + 4 * hh;  // 4 consecutive channels n..n+3
-        float v[4];
+        f16x4 v;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) v[t] = acc[4 * g + t] + (float)bias4[g][t];
+        for (int t = 0; t < 4; ++t) v[t] = lin_val(acc[4 * g + t], bias4[g][t]);
         if constexpr (EPI == EPI_BIAS) {
             if (p.res) {
 #pragma unroll
-                for (int t = 0; t < 4; ++t) v[t] += (float)aux0[g][t];
+                for (int t = 0; t < 4; ++t) v[t] = res_add(v[t], aux0[g][t]);
             }
-            *reinterpret_cast<f16x4*>(p.out[0] + (size_t)m * p.n + n) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+            *reinterpret_cast<f16x4*>(p.out[0] + (size_t)m * p.n + n) = v;
         } else {
             const int hd = p.heads * kD;
             const int part = n / hd, h = (n % hd) / kD, d = n % kD;
@@ -197,97 +217,13 @@ __global__ __launch_bounds__(256) void linear_kernel(LinArgs p) {
                 if (part < 2) {  // q, k: (x0, x1) -> (x0 c - x1 s, x1 c + x0 s), pairs (d, d+1)
                     const f16x4 cc = aux0[g], ss = aux1[g];
 #pragma unroll
-                    for (int t = 0; t < 4; t += 2) {
-                        const float x0 = v[t], x1 = v[t + 1];
-                        v[t] = x0 * (float)cc[t] - x1 * (float)ss[t];
-                        v[t + 1] = x1 * (float)cc[t + 1] + x0 * (float)ss[t + 1];
-                    }
+                    for (int t = 0; t < 4; t += 2) rot_pair(v, t, cc[t], ss[t], cc[t + 1], ss[t + 1]);
                 }
             }
             f16* dst = p.out[(first ? 0 : (EPI == EPI_QKV_ROTARY ? 3 : 1)) + (EPI == EPI_QKV_ROTARY ? part : 2 * part)];
-            *reinterpret_cast<f16x4*>(dst + lr.off + d) =
-                f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+            *reinterpret_cast<f16x4*>(dst + lr.off + d) = v;
         }
     }
-}
-
-// One lane's 4 consecutive output channels n..n+3 of activation row `row` (acc elements 4g..4g+3):
-// bias, then residual (EPI_BIAS) / rotary + per-image head-major scatter / head split.
-template <int EPI>
-__device__ __forceinline__ void epi_store(const LinArgs& p, int row, int n, const f32x16& acc, int g) {
-    const f16x4 b4 = *reinterpret_cast<const f16x4*>(p.bias + n);
-    float v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = acc[4 * g + u] + (float)b4[u];
-    if constexpr (EPI == EPI_BIAS) {
-        if (p.res) {
-            const f16x4 rr = *reinterpret_cast<const f16x4*>(p.res + (size_t)row * p.n + n);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] += (float)rr[u];
-        }
-        *reinterpret_cast<f16x4*>(p.out[0] + (size_t)row * p.n + n) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
-    } else {
-        const int hd = p.heads * kD;
-        const int part = n / hd, h = (n % hd) / kD, d = n % kD;
-        const LinRow lr = lin_row(p, row, h);
-        if constexpr (EPI == EPI_QKV_ROTARY) {
-            if (part < 2) {
-                const f16x4 cc = *reinterpret_cast<const f16x4*>(p.cosv + (size_t)row * kD + d);
-                const f16x4 ss = *reinterpret_cast<const f16x4*>(p.sinv + (size_t)row * kD + d);
-#pragma unroll
-                for (int u = 0; u < 4; u += 2) {
-                    const float x0 = v[u], x1 = v[u + 1];
-                    v[u] = x0 * (float)cc[u] - x1 * (float)ss[u];
-                    v[u + 1] = x1 * (float)cc[u + 1] + x0 * (float)ss[u + 1];
-                }
-            }
-        }
-        f16* dst = p.out[(lr.first ? 0 : (EPI == EPI_QKV_ROTARY ? 3 : 1)) + (EPI == EPI_QKV_ROTARY ? part : 2 * part)];
-        *reinterpret_cast<f16x4*>(dst + lr.off + d) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
-    }
-}
-
-// One 32 x 32 block of a 256-row form (lane = activation row `row`, channels nb0 + 8g + 4hh + t in
-// acc[4g + t]): with p.st16 and EPI_BIAS, v_permlane32_swap pairs (g, g + 1) between the two
-// half-waves so each lane stores 8 consecutive channels (16 B) per pair (lg_linear_cat 35.0 -> 32.3
-// us, lg_linear 23.7 -> 21.9 at P = 16; linear_ab_st16.jsonl); else epi_store per group.
-template <int EPI>
-__device__ __forceinline__ void epi_block(const LinArgs& p, int row, int nb0, const f32x16& acc, int hh) {
-    if constexpr (EPI == EPI_BIAS) {
-        if (p.st16) {
-            typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
-            typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
-            u32x2_ rk[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int n = nb0 + 8 * g + 4 * hh;
-                const f16x4 b4 = *reinterpret_cast<const f16x4*>(p.bias + n);
-                float v[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = acc[4 * g + u] + (float)b4[u];
-                if (p.res) {
-                    const f16x4 rr = *reinterpret_cast<const f16x4*>(p.res + (size_t)row * p.n + n);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) v[u] += (float)rr[u];
-                }
-                rk[g] = __builtin_bit_cast(u32x2_, f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]});
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k += 2) {
-#pragma unroll
-                for (int w = 0; w < 2; ++w) {
-                    const auto sw = __builtin_amdgcn_permlane32_swap(rk[k][w], rk[k + 1][w], false, false);
-                    rk[k][w] = sw[0];
-                    rk[k + 1][w] = sw[1];
-                }
-                *reinterpret_cast<u32x4_*>(p.out[0] + (size_t)row * p.n + nb0 + 8 * (k + hh)) =
-                    u32x4_{rk[k][0], rk[k][1], rk[k + 1][0], rk[k + 1][1]};
-            }
-            return;
-        }
-    }
-#pragma unroll
-    for (int g = 0; g < 4; ++g) epi_store<EPI>(p, row, nb0 + 8 * g + 4 * hh, acc, g);
 }
 
 // ---- per-tile DMA sources of the 256-row forms: each wave's W and A pieces of a tile, computed once
@@ -305,19 +241,20 @@ template <int BK>
 __device__ __forceinline__ int src_unit(int row, int pos) {
     return BK == 64 ? (pos ^ ((row >> 1) & 7)) : (pos ^ ((row >> 2) & 3));
 }
-template <bool GATHER, int BK, int NWP, int NAP>
+// (LW waves issue a stage's DMA pieces: piece wave + LW h)
+template <bool GATHER, int BK, int NWP, int NAP, int LW>
 __device__ __forceinline__ TileSrc<NWP, NAP> tile_src(const LinArgs& p, int m0, int n0, int wave, int lane) {
     constexpr int U = BK / 8, RP = 1024 / (2 * BK);
     TileSrc<NWP, NAP> t;
 #pragma unroll
     for (int h = 0; h < NWP; ++h) {
-        const int row = RP * (wave + 8 * h) + lane / U;
+        const int row = RP * (wave + LW * h) + lane / U;
         const int wr = min(n0 + row, p.n - 1);
         t.w[h] = p.w + (size_t)wr * p.k + src_unit<BK>(row, lane % U) * 8;
     }
 #pragma unroll
     for (int h = 0; h < NAP; ++h) {
-        const int row = RP * (wave + 8 * h) + lane / U;
+        const int row = RP * (wave + LW * h) + lane / U;
         const int ar = min(m0 + row, p.m - 1);
         const int gu8 = src_unit<BK>(row, lane % U) * 8;
         if constexpr (!GATHER) {
@@ -332,13 +269,13 @@ __device__ __forceinline__ TileSrc<NWP, NAP> tile_src(const LinArgs& p, int m0, 
     return t;
 }
 // K step ks (compile-time after unrolling; K = KS BK) of a tile into the stage at sb: W pieces
-// wave + 8h at sb, A pieces at sb + BN BK 2
-template <bool GATHER, int BK, int KS, int BN, int NWP, int NAP>
+// wave + LW h at sb, A pieces at sb + BN BK 2
+template <bool GATHER, int BK, int KS, int BN, int LW, int NWP, int NAP>
 __device__ __forceinline__ void tile_issue(const TileSrc<NWP, NAP>& t, int ks, char* sb, int wave) {
 #pragma unroll
     for (int h = 0; h < NWP; ++h)
         __builtin_amdgcn_global_load_lds((const void*)(t.w[h] + ks * BK),
-                                         (__attribute__((address_space(3))) void*)(sb + (wave + 8 * h) * 1024), 16, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(sb + (wave + LW * h) * 1024), 16, 0, 0);
 #pragma unroll
     for (int h = 0; h < NAP; ++h) {
         const f16* src;
@@ -350,303 +287,314 @@ __device__ __forceinline__ void tile_issue(const TileSrc<NWP, NAP>& t, int ks, c
             src = col < half ? t.a[h] + col : t.c[h] + ((col - half) / kD) * t.hs[h] + (col - half) % kD;
         }
         __builtin_amdgcn_global_load_lds((const void*)src,
-                                         (__attribute__((address_space(3))) void*)(sb + BN * BK * 2 + (wave + 8 * h) * 1024),
+                                         (__attribute__((address_space(3))) void*)(sb + BN * BK * 2 + (wave + LW * h) * 1024),
                                          16, 0, 0);
     }
 }
 
-// ---- the wide form, for launches with many rows (several image pairs per forward) ----
-// Workgroup: 256 rows (m) x 128 output channels (n) a tile, persistent over tiles (the DMA ring
-// runs on across tile seams: the next tile's first two K steps load during the current tile's
-// last two), 8 waves as 4 (m) x 2 (n) tiles of 64 x 64
-// (2 x 2 MFMA blocks of 32 x 32 each); K in 64-deep steps through a 3-stage LDS-DMA ring (48 KiB a
-// stage: W [128 rows][128 B] + A [256 rows][128 B], 16-B units XOR-swizzled by (row >> 1) & 7 on
-// the source address: conflict-free ds_read_b128 in every lane group), two steps in flight. Per
-// step and wave: 16 MFMA beside 16 fragment reads. The k16 blocks enter each accumulator in the
-// same order as in linear_kernel, so both forms give the same bits. Against the 64 x 64 form it
-// moves a quarter of the operand bytes per MAC out of L2 (128 KiB per 64 x 64 x 512 tile there).
-constexpr int kWM = 256, kWN = 128, kWK = 64;
-constexpr int kWStage = (kWM + kWN) * kWK * 2;  // 48 KiB
-constexpr int kWStages = 3;
-constexpr int kWGrid = 256;  // one workgroup per CU
-
-template <int EPI, bool GATHER, int KS>
-__global__ __launch_bounds__(512, 1) void linear_wide_kernel(LinArgs p) {
-    __shared__ __attribute__((aligned(16))) char smem[kWStages * kWStage];  // 144 KiB
+// ---- the 256-row forms, for launches with many rows (several image pairs per forward) ----
+// Persistent tiles of MT rows x NT channels (256 x 128, 256 x 256 or 128 x 256), 8 waves as WM (m) x
+// WN (n) tiles of 64 rows x NT / WN channels (2 x NB MFMA blocks of 32 x 32), K in BK-deep steps through
+// an NST-stage LDS-DMA ring (16-B units XOR-swizzled on the source address: conflict-free
+// ds_read_b128), NST - 1 steps in flight; the ring runs on across tile seams, so the next tile's
+// first steps load during the current tile's last ones. XCD-aware: the workgroups of XCD x walk the
+// contiguous tile range [jb, je) (tile j = m tile j / ntiles, n tile j % ntiles: the n tiles of one
+// m tile run side by side on one XCD and read its A rows through one L2).
+//
+// Epilogue (round 5): the MFMA layout puts one activation row on each lane, so stores straight from
+// the accumulators write 32 rows x 16-32 B per wave instruction; measured (ablations of the round-4
+// forms, profiles/r05/linear_ablations.jsonl) those stores cost more than the GEMM: lg_linear_qkv_rotary
+// 53.6 us with them, 15.9 without. Here each wave rounds (acc + bias) to fp16 into its own 4 KiB
+// region of the ring stage its tile's last K step has just freed (one barrier per tile), 32 rows x
+// 64 channels a round, reads it back row-major and writes whole 128-B row segments: 8 rows x 128 B
+// per wave instruction, the residual / rotary tables loaded in the same coalesced layout (prefetched
+// at the tile's last K step). The stores stay in flight into the next tile: its first NST - 1 waits
+// count them (every lane stores; rows past m are computed on the clamped last A row and write that
+// row's own bytes again, so the count is exact).
+// RES (EPI_BIAS): p.res is added (a compile-time form: its prefetch holds registers).
+template <int EPI, bool GATHER, bool RES, int KS, int MT, int NT, int BK, int NST>
+__global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
+    constexpr int WM = MT / 64, WN = 8 / WM, WTN = NT / WN, NB = WTN / 32, NP = WTN / 64;
+    constexpr int SB = (MT + NT) * BK * 2;                               // one ring stage
+    constexpr int NWP = NT * BK * 2 / 8192, NAP = MT * BK * 2 / 8192;    // 1-KiB DMA pieces per wave, step
+    constexpr int D = NWP + NAP;
+    constexpr int SPW = 2 * NP * 4;                                      // output stores per wave and tile
+    // epilogue operands loaded per wave and tile (at its first K step): bias, residual / cos + sin rows
+    constexpr int PF = NB * 4 + (RES ? 2 * NP * 4 : 0) + (EPI == EPI_QKV_ROTARY ? 16 : 0);
+    static_assert(SB >= 8 * 4096, "a staging region per wave inside one ring stage");
+    static_assert(KS >= NST - 1 && NB % 2 == 0 && (NST - 2) * D + SPW + PF <= 63, "shape");
+    static_assert(NB == 2 || (EPI != EPI_QKV_ROTARY && !RES), "64 x 128 wave tiles: no room for the prefetched tables");
+    __shared__ __attribute__((aligned(16))) char smem[NST * SB];
     lds_char* const lds = (lds_char*)smem;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave & 3, wn = wave >> 2;  // this wave's 64 x 64 tile of the 256 x 128
-    const int r = lane & 31, hh = lane >> 5;
-    // Persistent and XCD-aware: the workgroups of XCD x walk the contiguous tile range [jb, je)
-    // (tile j = m tile j / ntiles, n tile j % ntiles: the n tiles of one m tile run side by side
-    // on one XCD, so their A tile is read through one L2), every G-th tile from their local index.
-    const int T = p.total, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
-    const int q8 = T >> 3, r8 = T & 7;
-    const int jb = xcd * q8 + min(xcd, r8), je = jb + q8 + (xcd < r8 ? 1 : 0);
-    const int G = ((int)gridDim.x - xcd + 7) >> 3;
-    const int ntiles = p.n / kWN;
-    const int j0 = jb + loc;
-    if (j0 >= je) return;
-    const int ntile_w = (je - j0 + G - 1) / G;  // tiles of this workgroup
-    const int nsteps = ntile_w * KS;            // K steps over all of them
-
-    // DMA sources of this workgroup's tile t (computed once per tile)
-    auto src_of = [&](int t) {
-        const int jt = j0 + G * t, mt = jt / ntiles;
-        return tile_src<GATHER, kWK, 2, 4>(p, mt * kWM, (jt - mt * ntiles) * kWN, wave, lane);
-    };
-    TileSrc<2, 4> cur = src_of(0), nxt = cur;
-    tile_issue<GATHER, kWK, KS, kWN>(cur, 0, smem, wave);
-    tile_issue<GATHER, kWK, KS, kWN>(cur, 1, smem + kWStage, wave);
-
-    unsigned wro[2], aro[2];  // per block: row offset and swizzle key of this lane's fragment row
-    int wsw[2], asw[2];
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-        const int wrow = wn * 64 + 32 * b + r, arow = wm * 64 + 32 * b + r;
-        wro[b] = (unsigned)(wrow * 128), wsw[b] = (wrow >> 1) & 7;
-        aro[b] = (unsigned)(kWN * 128 + arow * 128), asw[b] = (arow >> 1) & 7;
-    }
-    int st = 0;  // stage of global step gs
-    for (int t = 0; t < ntile_w; ++t) {
-        const int jt = j0 + G * t;
-        const int mt = jt / ntiles, m0 = mt * kWM, n0 = (jt - mt * ntiles) * kWN;
-        const bool more = t + 1 < ntile_w;
-        if (more) nxt = src_of(t + 1);
-        f32x16 acc[2][2] = {};  // [n block][m block]
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            const int gs = t * KS + ks;
-            // step gs landed for this wave's 6 DMAs (step gs + 1's stay in flight), then for
-            // everyone's; after this barrier every wave is past step gs − 1, so its stage takes
-            // step gs + 2 (lgkmcnt(0): this wave's fragment reads of step gs − 1 are done)
-            if (gs + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            {
-                char* const fb = smem + (st == 0 ? 2 : st - 1) * kWStage;
-                if (ks + 2 < KS) tile_issue<GATHER, kWK, KS, kWN>(cur, ks + 2, fb, wave);
-                else if (more) tile_issue<GATHER, kWK, KS, kWN>(nxt, ks + 2 - KS, fb, wave);
-            }
-            const unsigned sb = (unsigned)(st * kWStage);
-            st = st == 2 ? 0 : st + 1;
-#pragma unroll
-            for (int s = 0; s < kWK / 16; ++s) {
-                f16x8 wf[2], af[2];
-#pragma unroll
-                for (int b = 0; b < 2; ++b) {
-                    const int u = 2 * s + hh;
-                    wf[b] = *(lds_f16x8*)(lds + sb + wro[b] + ((u ^ wsw[b]) << 4));
-                    af[b] = *(lds_f16x8*)(lds + sb + aro[b] + ((u ^ asw[b]) << 4));
-                }
-#pragma unroll
-                for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-                    for (int mb = 0; mb < 2; ++mb)
-                        acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[nb], af[mb], acc[nb][mb], 0, 0, 0);
-            }
-        }
-
-        // ---- epilogue: per (n block, m block), lane = activation row; acc[.][.][4g + t] =
-        // channel n0 + wn*64 + 32 nb + 8g + 4hh + t (the 64 x 64 form's epilogue per 32 x 32
-        // block). Its operand loads return after the next tile's first two DMA steps (issued
-        // above): the wait for them is the wait the next tile's first step makes anyway. ----
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            const int row = m0 + wm * 64 + 32 * mb + r;
-            if (row >= p.m) continue;
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) epi_block<EPI>(p, row, n0 + wn * 64 + 32 * nb, acc[nb][mb], hh);
-        }
-        cur = nxt;
-    }
-}
-
-// ---- the square form: 256 x 256 tiles, K in 32-deep steps through a 4-stage ring (32 KiB a
-// stage: W and A [256 rows][64 B], 16-B units XOR-swizzled by (row >> 2) & 3), three steps in
-// flight; 8 waves as 4 (m) x 2 (n) tiles of 64 rows x 128 channels (2 x 4 MFMA blocks). A step
-// stages 32 KiB for 4.2 MFLOP (the 256 x 128 form: 48 KiB). Same k16 order per accumulator as
-// the other forms: same bits. (lg_linear_set_wide(2) / LG_LINEAR_WIDE=2, where n % 256 == 0.)
-constexpr int kSM_ = 256, kSN = 256, kSK = 32;
-constexpr int kSStage = (kSM_ + kSN) * kSK * 2;  // 32 KiB
-
-// NST stages (4: 128 KiB; 5: the whole 160 KiB), NST − 1 steps in flight
-template <int EPI, bool GATHER, int KS, int NST>
-__global__ __launch_bounds__(512, 1) void linear_sq_kernel(LinArgs p) {
-    __shared__ __attribute__((aligned(16))) char smem[NST * kSStage];
-    lds_char* const lds = (lds_char*)smem;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave & 3, wn = wave >> 2;  // this wave's 64 x 128 tile of the 256 x 256
+    const int wm = wave % WM, wn = wave / WM;
     const int r = lane & 31, hh = lane >> 5;
     const int T = p.total, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
     const int q8 = T >> 3, r8 = T & 7;
     const int jb = xcd * q8 + min(xcd, r8), je = jb + q8 + (xcd < r8 ? 1 : 0);
     const int G = ((int)gridDim.x - xcd + 7) >> 3;
-    const int ntiles = p.n / kSN;
+    const int ntiles = p.n / NT;
     const int j0 = jb + loc;
     if (j0 >= je) return;
     const int ntile_w = (je - j0 + G - 1) / G;
     const int nsteps = ntile_w * KS;
 
-    // DMA sources of this workgroup's tile t (computed once per tile)
     auto src_of = [&](int t) {
         const int jt = j0 + G * t, mt = jt / ntiles;
-        return tile_src<GATHER, kSK, 2, 2>(p, mt * kSM_, (jt - mt * ntiles) * kSN, wave, lane);
+        return tile_src<GATHER, BK, NWP, NAP, 8>(p, mt * MT, (jt - mt * ntiles) * NT, wave, lane);
     };
-    TileSrc<2, 2> cur = src_of(0), nxt = cur;
+    TileSrc<NWP, NAP> cur = src_of(0), nxt = cur;
 #pragma unroll
-    for (int i = 0; i < NST - 1; ++i) tile_issue<GATHER, kSK, KS, kSN>(cur, i, smem + i * kSStage, wave);
+    for (int i = 0; i < NST - 1; ++i)
+        if constexpr (!(LG_ABL & 4)) tile_issue<GATHER, BK, KS, NT, 8>(cur, i, smem + i * SB, wave);
 
-    unsigned wro[4], aro[2];
-    int wsw[4], asw[2];
+    // fragment rows of this lane: W rows wn * WTN + 32 b + r, A rows wm * 64 + 32 b + r
+    auto swz = [](int row) { return BK == 64 ? (row >> 1) & 7 : (row >> 2) & 3; };
+    unsigned wro[NB], aro[2];
+    int wsw[NB], asw[2];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int wrow = wn * 128 + 32 * b + r;
-        wro[b] = (unsigned)(wrow * 64), wsw[b] = (wrow >> 2) & 3;
+    for (int b = 0; b < NB; ++b) {
+        const int wrow = wn * WTN + 32 * b + r;
+        wro[b] = (unsigned)(wrow * BK * 2), wsw[b] = swz(wrow);
     }
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
         const int arow = wm * 64 + 32 * b + r;
-        aro[b] = (unsigned)(kSN * 64 + arow * 64), asw[b] = (arow >> 2) & 3;
+        aro[b] = (unsigned)(NT * BK * 2 + arow * BK * 2), asw[b] = swz(arow);
     }
+    // coalesced phase: lane -> (row 8 i + lane / 8 of a 32-row round, 16-B chunk lane % 8 of 64 channels)
+    const int cr = lane >> 3, cc = lane & 7;
     int st = 0;
     for (int t = 0; t < ntile_w; ++t) {
         const int jt = j0 + G * t;
-        const int mt = jt / ntiles, m0 = mt * kSM_, n0 = (jt - mt * ntiles) * kSN;
+        const int mt = jt / ntiles, m0 = mt * MT, n0 = (jt - mt * ntiles) * NT;
+        const int nw0 = n0 + wn * WTN;  // this wave's first channel
         const bool more = t + 1 < ntile_w;
         if (more) nxt = src_of(t + 1);
-        f32x16 acc[4][2] = {};  // [n block][m block]
+        f32x16 acc[NB][2] = {};
+        f16x4 bias4[NB][4];
+        f16x8 aux[2][NP][4];  // residual rows (EPI_BIAS) / cos rows (QKV) of the coalesced phase
+        f16x8 aux2[2][4];     // sin rows (QKV)
+        int st_last = 0;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const int gs = t * KS + ks;
-            // step gs landed (up to NST − 2 later steps stay in flight: 4 DMAs each per wave),
-            // then everyone's; past this barrier every wave is done with step gs − 1's stage
-            const int later = min(NST - 2, nsteps - 1 - gs);
-            if (later >= 3) asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
-            else if (later == 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-            else if (later == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            {
-                char* const fb = smem + (st == 0 ? NST - 1 : st - 1) * kSStage;
-                if (ks + NST - 1 < KS) tile_issue<GATHER, kSK, KS, kSN>(cur, ks + NST - 1, fb, wave);
-                else if (more) tile_issue<GATHER, kSK, KS, kSN>(nxt, ks + NST - 1 - KS, fb, wave);
+            // step gs landed (this wave's pieces: younger ones = the later steps' DMAs in flight,
+            // plus the previous tile's output stores while they are younger), then everyone's; past
+            // this barrier every wave is done with step gs - 1's stage
+            // Younger than step gs's pieces: the later steps' DMA in flight; the previous tile's output
+            // stores while issued after gs's DMA (ks < NST - 1); this tile's epilogue operands,
+            // loaded at ks = 0 after that step's wait (1 <= ks <= NST - 2). (The workgroup's last
+            // NST - 2 steps have fewer later steps in flight: drain all.)
+            const bool pfk = ks >= 1 && ks <= NST - 2;  // (folded after unrolling)
+            if (gs + NST - 2 > nsteps - 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            else if (ks < NST - 1 && t > 0) {
+                if (pfk) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * D + SPW + PF) : "memory");
+                else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * D + SPW) : "memory");
+            } else {
+                if (pfk) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * D + PF) : "memory");
+                else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * D) : "memory");
             }
-            const unsigned sb = (unsigned)(st * kSStage);
+            __builtin_amdgcn_s_barrier();
+            if (ks == 0) {
+                // the epilogue's operands, a whole tile ahead of their use (rows clamped to m - 1, as
+                // the A rows are; the rotary tables for the v part too: a fixed count for the waits)
+#pragma unroll
+                for (int b = 0; b < NB; ++b)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        bias4[b][g] = *reinterpret_cast<const f16x4*>(p.bias + nw0 + 32 * b + 8 * g + 4 * hh);
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = min(m0 + wm * 64 + 32 * mb + 8 * i + cr, p.m - 1);
+                        if constexpr (EPI == EPI_BIAS && RES) {
+#pragma unroll
+                            for (int np = 0; np < NP; ++np)
+                                aux[mb][np][i] = *reinterpret_cast<const f16x8*>(p.res + (size_t)row * p.n + nw0 + 64 * np + 8 * cc);
+                        } else if constexpr (EPI == EPI_QKV_ROTARY) {
+                            aux[mb][0][i] = *reinterpret_cast<const f16x8*>(p.cosv + (size_t)row * kD + 8 * cc);
+                            aux2[mb][i] = *reinterpret_cast<const f16x8*>(p.sinv + (size_t)row * kD + 8 * cc);
+                        }
+                    }
+            }
+            {
+                char* const fb = smem + (st == 0 ? NST - 1 : st - 1) * SB;
+                if (LG_ABL & 4) {
+                } else if (ks + NST - 1 < KS) tile_issue<GATHER, BK, KS, NT, 8>(cur, ks + NST - 1, fb, wave);
+                else if (more) tile_issue<GATHER, BK, KS, NT, 8>(nxt, ks + NST - 1 - KS, fb, wave);
+            }
+            const unsigned sb = (unsigned)(st * SB);
+            st_last = st;
             st = st == NST - 1 ? 0 : st + 1;
 #pragma unroll
-            for (int s = 0; s < kSK / 16; ++s) {
+            for (int s = 0; s < BK / 16; ++s) {
                 const int u = 2 * s + hh;
-                f16x8 wf[4], af[2];
+                f16x8 wf[NB], af[2];
 #pragma unroll
-                for (int b = 0; b < 4; ++b) wf[b] = *(lds_f16x8*)(lds + sb + wro[b] + ((u ^ wsw[b]) << 4));
+                for (int b = 0; b < NB; ++b) wf[b] = *(lds_f16x8*)(lds + sb + wro[b] + ((u ^ wsw[b]) << 4));
 #pragma unroll
                 for (int b = 0; b < 2; ++b) af[b] = *(lds_f16x8*)(lds + sb + aro[b] + ((u ^ asw[b]) << 4));
 #pragma unroll
-                for (int nb = 0; nb < 4; ++nb)
+                for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
                     for (int mb = 0; mb < 2; ++mb)
-                        acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[nb], af[mb], acc[nb][mb], 0, 0, 0);
+                        if constexpr (!(LG_ABL & 2))
+                            acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[nb], af[mb], acc[nb][mb], 0, 0, 0);
             }
         }
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            const int row = m0 + wm * 64 + 32 * mb + r;
-            if (row >= p.m) continue;
-#pragma unroll
-            for (int nb = 0; nb < 4; ++nb) epi_block<EPI>(p, row, n0 + wn * 128 + 32 * nb, acc[nb][mb], hh);
+
+        // ---- epilogue: the operands loaded at ks = 0 landed (younger: this tile's KS DMA issues when
+        // another tile follows; a count capped at 63 only waits for more); every wave's fragment reads
+        // of the last stage done (barrier) ----
+        if (more) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KS * D < 63 ? KS * D : 63) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        lds_char* const stg = lds + st_last * SB + wave * 4096;
+        if constexpr (LG_ABL & 1) {
+            if (p.m != -12345) continue;
         }
+        const int hd = p.heads * kD;
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+            for (int np = 0; np < NP; ++np) {
+                // (acc + bias) -> fp16, rows r of the round, 16-B chunk (4 nbl + g) ^ (r & 7), half hh
+#pragma unroll
+                for (int nbl = 0; nbl < 2; ++nbl)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const f32x16& a = acc[2 * np + nbl][mb];
+                        const f16x4 b4 = bias4[2 * np + nbl][g];
+                        const f16x4 v = f16x4{lin_val(a[4 * g], b4[0]), lin_val(a[4 * g + 1], b4[1]),
+                                              lin_val(a[4 * g + 2], b4[2]), lin_val(a[4 * g + 3], b4[3])};
+                        *(__attribute__((address_space(3))) f16x4*)(stg + r * 128 + (((4 * nbl + g) ^ (r & 7)) << 4) + 8 * hh) = v;
+                    }
+                f16x8 o[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rl = 8 * i + cr;
+                    o[i] = *(lds_f16x8*)(stg + rl * 128 + ((cc ^ (rl & 7)) << 4));
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = min(m0 + wm * 64 + 32 * mb + 8 * i + cr, p.m - 1);
+                    const int n = nw0 + 64 * np + 8 * cc;  // 8 consecutive channels n..n+7
+                    f16x8 v = o[i];
+                    if constexpr (EPI == EPI_BIAS) {
+                        if constexpr (RES) {
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], aux[mb][np][i][e]);
+                        }
+                        *reinterpret_cast<f16x8*>(p.out[0] + (size_t)row * p.n + n) = v;
+                    } else {
+                        const int part = n / hd, h = (n % hd) / kD, d = n % kD;
+                        if constexpr (EPI == EPI_QKV_ROTARY) {
+                            if (part < 2) {
+#pragma unroll
+                                for (int e = 0; e < 8; e += 2)
+                                    rot_pair(v, e, aux[mb][0][i][e], aux2[mb][i][e], aux[mb][0][i][e + 1], aux2[mb][i][e + 1]);
+                            }
+                        }
+                        const LinRow lr = lin_row(p, row, h);
+                        f16* dst = p.out[(lr.first ? 0 : (EPI == EPI_QKV_ROTARY ? 3 : 1)) + (EPI == EPI_QKV_ROTARY ? part : 2 * part)];
+                        *reinterpret_cast<f16x8*>(dst + lr.off + d) = v;
+                    }
+                }
+            }
         cur = nxt;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// The wide form where it fills the chip: at least one round of its 256 x 128 tiles (n a multiple of
-// 128). lg_linear_set_wide(0 / 1) or LG_LINEAR_WIDE=0 / 1 forces it off / on (where n allows), for
-// tests and A/B timing; -1 (the default) chooses by size.
+constexpr int kTileGrid = 256;  // the 256-row forms: one workgroup per CU
+// The tile form (tile_form below): lg_linear_set_wide(0..3) or LG_LINEAR_WIDE forces one (where n
+// allows), for tests and A/B timing; -1 (the default) chooses by size.
 std::atomic<int> g_wide{-2};
 int wide_mode() {
     int v = g_wide.load();
     if (v == -2) {
         const char* e = std::getenv("LG_LINEAR_WIDE");
+        long m = -1;  // unset or unparsable: chosen by size
+        if (e && *e) {
+            char* end = nullptr;
+            const long x = std::strtol(e, &end, 10);
+            if (end != e) m = x < -1 ? -1 : (x > 3 ? 3 : x);
+        }
         int expect = -2;
-        g_wide.compare_exchange_strong(expect, e ? (e[0] == '2' ? 2 : e[0] == '1' ? 1 : 0) : -1);
+        g_wide.compare_exchange_strong(expect, (int)m);
         v = g_wide.load();
     }
     return v;
 }
-bool use_wide(const LinArgs& p) {
-    if (p.n % kWN) return false;
+bool aligned16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+bool aligned8(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 7) == 0; }
+
+// The 256-row tile forms (linear_tile_kernel): 1 = 256 x 128, 2 = 256 x 256 (32-deep K steps, 4
+// stages; plain EPI_BIAS only: the residual / rotary tables and the scatter addressing do not fit
+// beside its accumulators), 3 = 128 x 256. Forced by lg_linear_set_wide / LG_LINEAR_WIDE where n and the operand
+// alignment allow, else chosen by size: 256 x 128 tiles from half a round (128) of them on (at
+// P = 4 pairs, M = 8,192: qkv 12.5 vs 20.2 us, cat 11.5 vs 19.0, split2 / linear even; below, the
+// 64 x 64 form's more workgroups win; profiles/r05/linear_ab_tile_forms.jsonl).
+int tile_form(const LinArgs& p, int epi) {
+    bool al = aligned16(p.bias);
+    const int nout = epi == EPI_BIAS ? 1 : epi == EPI_QKV_ROTARY ? 6 : 4;
+    for (int i = 0; i < nout; ++i) al = al && aligned16(p.out[i]);
+    if (p.res) al = al && aligned16(p.res);
+    if (epi == EPI_QKV_ROTARY) al = al && aligned16(p.cosv) && aligned16(p.sinv);
+    if (!al) return 0;
     const int w = wide_mode();
-    if (w >= 0) return w >= 1;
-    return (long)((p.m + kWM - 1) / kWM) * (p.n / kWN) >= 256;
-}
-// the square form: forced (mode 2), or by size where its tiles fill whole rounds of the chip
-// (N = 512 at P = 16, N = 1024: cat 36.5 -> 33.2 us, cross qk|v 27.5 -> 25.1; N = 256 / 768 take
-// half / one and a half rounds of it and stay on the 256 x 128 form; linear_ab_square.jsonl)
-bool use_sq(const LinArgs& p) {
-    if (p.n % kSN) return false;
-    const int w = wide_mode();
-    if (w >= 0) return w >= 2;
-    const long t = (long)((p.m + kSM_ - 1) / kSM_) * (p.n / kSN);
-    return t >= kWGrid && (t % kWGrid == 0 || t >= 4 * kWGrid);
+    const int f = w >= 0 ? w : ((long)((p.m + 255) / 256) * (p.n / 128) >= 128 ? 1 : 0);
+    if (f == 1 && p.n % 128 == 0) return 1;
+    if (f == 2 && p.n % 256 == 0) return (p.res || epi != EPI_BIAS) ? 1 : 2;
+    if (f == 3 && p.n % 256 == 0) return 3;
+    return f >= 1 && p.n % 128 == 0 ? 1 : 0;
 }
 
-int st16_env() {
-    static const int v = [] {
-        const char* e = std::getenv("LG_LINEAR_ST16");  // (0: the per-group 8-B stores)
-        return (e && e[0] == '0') ? 0 : 1;
-    }();
-    return v;
+template <int EPI, bool GATHER, bool RES, int MT, int NT, int BK, int NST>
+void launch_tile_r(LinArgs& p, hipStream_t stream) {
+    p.mtiles = (p.m + MT - 1) / MT;
+    p.total = p.mtiles * (p.n / NT);
+    const int grid = p.total < kTileGrid ? p.total : kTileGrid;  // persistent: one round
+    if (p.k == 256)
+        hipLaunchKernelGGL((linear_tile_kernel<EPI, GATHER, RES, 256 / BK, MT, NT, BK, NST>), dim3(grid), dim3(512), 0, stream, p);
+    else
+        hipLaunchKernelGGL((linear_tile_kernel<EPI, GATHER, RES, 512 / BK, MT, NT, BK, NST>), dim3(grid), dim3(512), 0, stream, p);
+}
+template <int EPI, bool GATHER, int MT, int NT, int BK, int NST>
+void launch_tile(LinArgs& p, hipStream_t stream) {
+    constexpr bool WIDE_WAVE = NT * MT / 64 / 8 / 32 > 2;  // 64 x 128 wave tiles
+    if constexpr (EPI == EPI_BIAS && !GATHER && !WIDE_WAVE) {
+        if (p.res) return launch_tile_r<EPI, GATHER, true, MT, NT, BK, NST>(p, stream);
+    }
+    if constexpr (!(WIDE_WAVE && EPI == EPI_QKV_ROTARY)) launch_tile_r<EPI, GATHER, false, MT, NT, BK, NST>(p, stream);
 }
 
 template <int EPI, bool GATHER>
 int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
-    p.st16 = st16_env();
-    if (use_sq(p)) {
-        p.mtiles = (p.m + kSM_ - 1) / kSM_;
-        p.total = p.mtiles * (p.n / kSN);
-        const int grid = p.total < kWGrid ? p.total : kWGrid;
-        if (wide_mode() == 3) {  // (A/B: five stages)
+    int form = tile_form(p, EPI);
+    if (GATHER && form == 2) form = 1;  // (the gather's per-piece sources do not fit beside 64 x 128 wave tiles)
+    switch (form) {
+        case 1: launch_tile<EPI, GATHER, 256, 128, 64, 3>(p, stream); break;
+        case 2:
+            if constexpr (!GATHER && EPI == EPI_BIAS) launch_tile<EPI, GATHER, 256, 256, 32, 4>(p, stream);
+            break;
+        case 3: launch_tile<EPI, GATHER, 128, 256, 64, 3>(p, stream); break;
+        default:
+            p.mtiles = (p.m + kBM - 1) / kBM;
+            p.total = p.mtiles * (p.n / kBN);
             if (p.k == 256)
-                hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 8, 5>), dim3(grid), dim3(512), 0, stream, p);
+                hipLaunchKernelGGL((linear_kernel<EPI, GATHER, 2>), dim3(p.total), dim3(256), 0, stream, p);
             else
-                hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 16, 5>), dim3(grid), dim3(512), 0, stream, p);
-        } else if (p.k == 256) {
-            hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 8, 4>), dim3(grid), dim3(512), 0, stream, p);
-        } else {
-            hipLaunchKernelGGL((linear_sq_kernel<EPI, GATHER, 16, 4>), dim3(grid), dim3(512), 0, stream, p);
-        }
-        const hipError_t e = hipGetLastError();
-        return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
-                               : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, what, hipGetErrorString(e));
+                hipLaunchKernelGGL((linear_kernel<EPI, GATHER, 4>), dim3(p.total), dim3(256), 0, stream, p);
     }
-    if (use_wide(p)) {
-        p.mtiles = (p.m + kWM - 1) / kWM;
-        p.total = p.mtiles * (p.n / kWN);
-        const int grid = p.total < kWGrid ? p.total : kWGrid;  // persistent: one round
-        if (p.k == 256)
-            hipLaunchKernelGGL((linear_wide_kernel<EPI, GATHER, 4>), dim3(grid), dim3(512), 0, stream, p);
-        else
-            hipLaunchKernelGGL((linear_wide_kernel<EPI, GATHER, 8>), dim3(grid), dim3(512), 0, stream, p);
-        const hipError_t e = hipGetLastError();
-        return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
-                               : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, what, hipGetErrorString(e));
-    }
-    p.mtiles = (p.m + kBM - 1) / kBM;
-    p.total = p.mtiles * (p.n / kBN);
-    if (p.k == 256)
-        hipLaunchKernelGGL((linear_kernel<EPI, GATHER, 2>), dim3(p.total), dim3(256), 0, stream, p);
-    else
-        hipLaunchKernelGGL((linear_kernel<EPI, GATHER, 4>), dim3(p.total), dim3(256), 0, stream, p);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, what, hipGetErrorString(e));
 }
 
-bool aligned16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
-bool aligned8(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 7) == 0; }
 bool shape_ok(int m, int n, int k) { return m >= 0 && n > 0 && n % kBN == 0 && (k == 256 || k == 512); }
 
 int32_t bad(const char* what) { return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, what, "bad arguments"); }
@@ -718,5 +666,7 @@ int32_t lg_linear_set_wide(int32_t mode) {
     wide_mode();
     return g_wide.exchange(mode < 0 ? -1 : (mode > 3 ? 3 : mode));
 }
+
+int32_t lg_glue_abi_version(void) { return LG_GLUE_ABI_VERSION; }
 
 }  // extern "C"

@@ -138,6 +138,7 @@ SIGNATURES.update({
     "lg_log_double_softmax_workspace": ([_I, _I, _I], _S),
     "lg_log_double_softmax": ([_P, _P, _P, _I, _I, _I, _P, _P, _P], _I),
     "lg_linear_set_wide": ([_I], _I),
+    "lg_glue_abi_version": ([], _I),
     # kernel-form switches (include/mha_hd64.h "kernel-form switches")
     "mha_hd64_set_fused_combine": ([_I], None),
     "mha_hd64_set_f32_inkernel": ([_I], None),
@@ -155,6 +156,9 @@ _lib = None
 
 class LibraryMissing(RuntimeError):
     pass
+
+
+GLUE_ABI_VERSION = 2  # include/lightglue_glue.h LG_GLUE_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:
@@ -177,6 +181,8 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = res
+    if lib.lg_glue_abi_version() != GLUE_ABI_VERSION:  # the argument lists below match ABI 2 only
+        raise LibraryMissing(f"{LIB_PATH}: glue ABI {lib.lg_glue_abi_version()}, this package binds {GLUE_ABI_VERSION}")
     _lib = lib
     return lib
 

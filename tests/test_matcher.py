@@ -259,11 +259,18 @@ SWEEP = json.load(open(os.path.join(GOLD, "matcher_sweep_index.json")))
 SWEEP_TOL = {"float32": (1e-2, 1e-1, 5e-4), "float16": (6e-2, 0.6, 5e-3)}
 SWEEP_RECALL = 0.9
 # |log-score - reference| on the reference's mutual nearest neighbours (every threshold-0 match: the
-# entries that decide matching), ~3x the largest error observed on MI355X over the sweep sizes
-# (printed by the tests, round 4): fp32 2.0e-2, fp16 0.16 for one pair per forward; inside a batch
-# of pairs the attention launches take other plans (the streaming kernel) and fp16 reaches 0.28
+# entries that decide matching). The fp16 value is not a property of one attention plan: nine fp16
+# layers amplify any rounding difference, and perturbing each attention output by +-1 fp16 ulp on a
+# random 10 % of its elements (tools/matcher_plan_errors.py, profiles/r05/matcher_plan_errors*.jsonl,
+# 1024 x 1024 fixture) moves this error over 0.14-0.26 across 8 seeds; one pair per forward under
+# other attention plans 0.15-0.21, the fixture pair inside P = 4 / 8 pairs per forward (stream modes
+# 0 and 1) 0.135-0.20. fp32: 0.011-0.022. Bounds ~2x the largest of those.
 SWEEP_TOL_MATCHED = {"float32": 6e-2, "float16": 0.5}
-SWEEP_TOL_MATCHED_BATCHED = {"float32": 6e-2, "float16": 0.85}
+SWEEP_TOL_MATCHED_BATCHED = SWEEP_TOL_MATCHED
+# A batched forward against the same pair's own forward, every element: two fp16 forwards differ by
+# what a 1-ulp attention perturbation alone moves (same tool: descriptors 0.039, log-scores 0.525 over
+# 8 seeds; batched vs single measured 0.031 / 0.511); fp32 ~10x tighter. Bounds ~2x those.
+BATCHED_VS_SINGLE = {"float32": (1e-2, 1e-1), "float16": (8e-2, 1.0)}
 
 
 def _sweep_model(name, attention=None, glue="hip"):
@@ -381,7 +388,7 @@ def test_batched_pairs_equal_single_pair_forwards(pairs, dtype):
         singles = [model(*(t.to(dev, dt) for t in p)) for p in ps]
         torch.cuda.synchronize()
     assert bsc.shape == (pairs, meta["m"], meta["n"])
-    tol_d, tol_s, _ = SWEEP_TOL[dtype]
+    tol_d, tol_s = BATCHED_VS_SINGLE[dtype]
     worst = [0.0, 0.0]
     for i, (d0, d1, sc) in enumerate(singles):
         ed = max(float((bd0[i] - d0[0]).abs().max()), float((bd1[i] - d1[0]).abs().max()))
@@ -488,11 +495,12 @@ def test_torch_glue_runs_pairs_one_by_one():
 @pytest.mark.gpu
 @pytest.mark.parametrize("pairs,n0,n1", [(3, 37, 70), (2, 1000, 777), (16, 1024, 1024)])
 def test_wide_projections_equal_narrow(pairs, n0, n1):
-    """The projections' 256 x 128-tile and 256 x 256-tile forms (csrc/lightglue_linear.hip linear_wide_kernel /
-    linear_sq_kernel, taken for
-    launches of at least one round of its tiles: several image pairs per forward) gives the bits of
-    the 64 x 64 form on every fused entry point — ragged row counts (rows past m in a tile), both
-    K (256 and 512), residual on and off, the A-gather of lg_linear_cat, the per-image scatters."""
+    """The projections' 256-row tile forms (csrc/lightglue_linear.hip linear_tile_kernel: 256 x 128,
+    256 x 256 and 128 x 256 tiles with the LDS-staged coalesced epilogue, taken for launches of at
+    least one round of tiles: several image pairs per forward) give the bits of the 64 x 64 form on
+    every fused entry point — ragged row counts (rows past m in a tile: computed on the clamped last
+    row, their stores rewrite that row's bytes), both K (256 and 512), residual on and off, the
+    A-gather of lg_linear_cat, the per-image scatters."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from lightglue_amd import _lib
@@ -528,13 +536,14 @@ def test_wide_projections_equal_narrow(pairs, n0, n1):
         prev = lib.lg_linear_set_wide(0)
         try:
             narrow = [flat(o) for o in run()]
-            lib.lg_linear_set_wide(1)
-            wide = [flat(o) for o in run()]
-            lib.lg_linear_set_wide(2)  # 256 x 256 tiles, 32-deep K steps
-            square = [flat(o) for o in run()]
+            forms = []
+            for mode in (1, 2, 3):  # 256 x 128; 256 x 256 (32-deep K steps); 128 x 256
+                lib.lg_linear_set_wide(mode)
+                forms.append([flat(o) for o in run()])
             torch.cuda.synchronize()
         finally:
             lib.lg_linear_set_wide(prev)
-        for a, b, c in zip(narrow, wide, square):
-            for ta, tb, tc in zip(a, b, c):
-                assert torch.equal(ta, tb) and torch.equal(ta, tc)
+        for f, form in enumerate(forms):
+            for i, (a, b) in enumerate(zip(narrow, form)):
+                for ta, tb in zip(a, b):
+                    assert torch.equal(ta, tb), (f + 1, i, float((ta.float() - tb.float()).abs().max()))

@@ -2,7 +2,11 @@
 256 x 128-tile and 256 x 256-tile forms (lg_linear_set_wide 0 / 1 / 2) at P image pairs of n keypoints per image, graph
 replay of back-to-back launches, interleaved; TFLOP/s of each.
 
-    python tools/linear_ab.py [P] [n] [op substring] [modes, e.g. 012]"""
+    python tools/linear_ab.py [P] [n] [op substring] [modes, e.g. 012] [b]
+
+With a fifth argument "b": yardsticks in the same run -- torch.nn.functional.linear (hipBLASLt,
+fp16, plain [M, N] output + bias) on the op's M / K / N, and a device copy of the op's algorithmic
+bytes (its HBM roofline at the copy rate); yardsticks only, never a product path."""
 import json
 import os
 import statistics
@@ -20,7 +24,8 @@ def main():
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 16
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
     only = sys.argv[3] if len(sys.argv) > 3 else ""  # op-name substring (counter runs)
-    modes = tuple(int(c) for c in sys.argv[4]) if len(sys.argv) > 4 else (0, 1, 2)
+    modes = tuple(int(c) for c in sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4] else (0, 1, 2)
+    yard = len(sys.argv) > 5 and sys.argv[5] == "b"
     lib = _lib.load()
     dev, dt, h = torch.device("cuda:0"), torch.float16, 4
     M = P * 2 * n
@@ -40,6 +45,23 @@ def main():
         "cat k512 n512": (lambda: mt._Hip.linear_cat(x, c0, c1, w3, b3), 512 * 512),
         "linear+res k512 n256": (lambda: mt._Hip.linear(hx, w4, b4, x), 512 * 256),
     }
+    # algorithmic bytes per op: A + W + bias + outputs (+ cos/sin, + residual)
+    nbytes = {
+        "qkv_rotary k256 n768": 2 * (M * 256 + 768 * 256 + 768 + M * 768 + 2 * M * 64),
+        "split2 k256 n512": 2 * (M * 256 + 512 * 256 + 512 + M * 512),
+        "cat k512 n512": 2 * (M * 512 + 512 * 512 + 512 + M * 512),
+        "linear+res k512 n256": 2 * (M * 512 + 256 * 512 + 256 + 2 * M * 256),
+    }
+    blas = {}
+    if yard:
+        xa, xb = x.view(M, 256), hx.view(M, 512)
+        blas = {
+            "qkv_rotary k256 n768": lambda: torch.nn.functional.linear(xa, w768, b768),
+            "split2 k256 n512": lambda: torch.nn.functional.linear(xa, w2, b2),
+            "cat k512 n512": lambda: torch.nn.functional.linear(xb, w3, b3),
+            "linear+res k512 n256": lambda: torch.nn.functional.linear(xb, w4, b4),
+        }
+        pool = torch.empty(2 * max(nbytes.values()) // 2 + 16, dtype=torch.uint8, device=dev)
     st = torch.cuda.Stream(dev)
     K = 20
     graphs = {}
@@ -54,6 +76,17 @@ def main():
                     for _ in range(K):
                         fn()
             graphs[(name, wide)] = g
+        if yard:
+            half = nbytes[name] // 2 // 16 * 16
+            src_, dst_ = pool[:half], pool[half:2 * half]
+            for key, fn_ in (("blas", blas[name]), ("copy", lambda: dst_.copy_(src_))):
+                with torch.cuda.stream(st):
+                    fn_()
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=st):
+                        for _ in range(K):
+                            fn_()
+                graphs[(name, key)] = g
     lib.lg_linear_set_wide(-1)
     torch.cuda.synchronize()
     times = {k: [] for k in graphs}
@@ -71,6 +104,12 @@ def main():
         for wide in modes:
             us = statistics.median(times[(name, wide)])
             row[("narrow", "wide", "square", "square5")[wide]] = {"us": round(us, 2), "tflops": round(2.0 * M * kn / us / 1e6, 1)}
+        row["alg_MB"] = round(nbytes[name] / 1e6, 2)
+        if yard:
+            us = statistics.median(times[(name, "blas")])
+            row["hipblaslt_F_linear"] = {"us": round(us, 2), "tflops": round(2.0 * M * kn / us / 1e6, 1)}
+            us = statistics.median(times[(name, "copy")])
+            row["copy_alg_bytes"] = {"us": round(us, 2), "TB_s": round(nbytes[name] / us / 1e6, 2)}
         print(json.dumps(row), flush=True)
 
 

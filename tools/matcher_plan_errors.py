@@ -54,11 +54,20 @@ def main():
     model, pair = tm._sweep_model(NAME)
     model = model.to(dev, dt)
 
+    base = {}
+
     def run(m, inputs, slot=0):
         with torch.no_grad():
             d0, d1, sc = m(*(t.to(dev, dt) for t in inputs))
             torch.cuda.synchronize()
-        return errs(g, *(t[slot:slot + 1].float().cpu() for t in (d0, d1, sc)))
+        outs = tuple(t[slot:slot + 1].float().cpu() for t in (d0, d1, sc))
+        e = errs(g, *outs)
+        if base:  # against the default single-pair forward, every element (test_matcher's batched-vs-single check)
+            e["vs_single_desc"] = round(max(float((outs[0] - base["d0"]).abs().max()), float((outs[1] - base["d1"]).abs().max())), 5)
+            e["vs_single_scores"] = round(float((outs[2] - base["sc"]).abs().max()), 4)
+        else:
+            base.update(d0=outs[0], d1=outs[1], sc=outs[2])
+        return e
 
     def out(kind, **kw):
         print(json.dumps({"dtype": dtype, "kind": kind, **kw}), flush=True)
@@ -103,14 +112,17 @@ def main():
             return res
         return attn
 
-    ms = []
+    ms, vs, vd = [], [], []
     for seed in range(8):
         model.attention = perturbed(seed)
         e = run(model, pair)
         ms.append(e["matched"])
+        vs.append(e["vs_single_scores"])
+        vd.append(e["vs_single_desc"])
         out("ulp", seed=seed, **e)
     model.attention = base_attn
-    out("ulp_summary", matched_min=min(ms), matched_max=max(ms), matched_median=float(np.median(ms)))
+    out("ulp_summary", matched_min=min(ms), matched_max=max(ms), matched_median=float(np.median(ms)),
+        vs_single_scores_max=max(vs), vs_single_desc_max=max(vd))
     lightglue_amd.set_stream_mode(prev_mode)
 
 
