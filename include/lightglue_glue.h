@@ -78,6 +78,15 @@ int32_t lg_linear(const void* a, const void* w, const void* bias, const void* re
  *                       ctx_i [heads, ni, 64] (k = 2*heads*64; the FFN input of lightglue.py:104/181). */
 int32_t lg_linear_cat(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
                       int32_t pairs, const void* w, const void* bias, int32_t n, void* out, hipStream_t stream);
+/* lg_linear_cat_ln_gelu: the FFN's first half (lightglue.py:101-106) after lg_linear_cat:
+ *                       out [n0+n1, 512] = GELU(LayerNorm(fp16([x | merge_heads(ctx0, ctx1)] · Wᵀ + bias)))
+ *                       with the LayerNorm's gamma, beta [512] and eps (exact-erf GELU). heads * 128 must
+ *                       be 512 for the one-launch form (128-row tiles owning whole rows; opt-in, see
+ *                       lg_linear_set_ln_fused; from 128 tiles on, 16-B aligned bias / gamma / beta / out);
+ *                       otherwise (the default) lg_linear_cat then lg_layernorm_gelu in place. */
+int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
+                              int32_t pairs, const void* w, const void* bias, const void* gamma, const void* beta,
+                              float eps, void* out, hipStream_t stream);
 /* lg_linear_qkv_rotary: SelfBlock projection (lightglue.py:111-134) with W's rows and the bias in
  *                       [q|k|v][head][dim] order (row j*heads*64 + h*64 + d = Wqkv row (h*64+d)*3 + j):
  *                       rotary (cos/sin [n0+n1, 64]) on q and k, per-image head-major outputs. */
@@ -104,6 +113,11 @@ int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1
  * LG_LINEAR_WIDE sets the initial mode the same way. Every form gives the same bits. Returns the
  * previous mode. */
 int32_t lg_linear_set_wide(int32_t mode);
+
+/* Test and benchmark hook: 1 lets lg_linear_cat_ln_gelu take its one-launch form where it applies
+ * (default 0: measured slower, csrc/lightglue_linear.hip). Same results within fp16 rounding, not the
+ * same bits (its variance is two-pass). Returns the previous setting. */
+int32_t lg_linear_set_ln_fused(int32_t on);
 
 #ifdef __cplusplus
 }

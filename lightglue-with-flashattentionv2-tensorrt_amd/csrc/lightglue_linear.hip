@@ -103,6 +103,20 @@ __device__ __forceinline__ const f16* a_src(const LinArgs& p, int row, int gc) {
 // fp16 model does (x + ffn(...), q * cos + rotate(q) * sin), in fp32 with one rounding each.
 __device__ __forceinline__ f16 lin_val(float acc, f16 b) { return (f16)(acc + (float)b); }
 __device__ __forceinline__ f16 res_add(f16 v, f16 r) { return (f16)((float)v + (float)r); }
+// erf for the fp16 GELU: Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), as lightglue_glue.hip's
+// LayerNorm+GELU kernel computes it
+__device__ __forceinline__ float erf_as(float x) {
+    const float a = fabsf(x);
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+    float y = fmaf(1.061405429f, t, -1.453152027f);
+    y = fmaf(y, t, 1.421413741f);
+    y = fmaf(y, t, -0.284496736f);
+    y = fmaf(y, t, 0.254829592f);
+    y *= t;
+    const float e = 1.f - y * __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);
+    return copysignf(e, x);
+}
+
 // (x0, x1) of a rotary pair (d, d + 1) -> (x0 c0 - x1 s0, x1 c1 + x0 s1), elements e, e + 1 of v
 template <typename V>
 __device__ __forceinline__ void rot_pair(V& v, int e, f16 c0, f16 s0, f16 c1, f16 s1) {
@@ -509,7 +523,203 @@ __global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---- the FFN input projection with LayerNorm + GELU in its epilogue (lg_linear_cat_ln_gelu) ----
+// LightGlue's FFN (lightglue.py:101-106) is Linear(2d, 2d) -> LayerNorm(2d) -> GELU -> Linear(2d, d):
+// lg_linear_cat writes h = [x | heads]·Wᵀ + b, a separate pass normalises it (17 us at P = 16, M =
+// 32,768: 33.5 MB read, 33.5 MB written; profiles/r05/matcher_p16_kernel_stats_tile_forms_v1.csv).
+// Here a workgroup owns whole rows: tiles of 128 rows x all 512 channels (8 waves as 2 (m) x 4 (n)
+// tiles of 64 x 128; K in 32-deep steps through a 3-stage LDS-DMA ring of 40 KiB stages, the A-gather
+// of lg_linear_cat), so the row statistics close inside the workgroup: h = fp16(acc + bias) as the
+// unfused path rounds it, row sums per wave -> LDS -> mean; sums of (h - mean)^2 -> LDS -> variance
+// (two passes over registers: the unfused kernel's E[h^2] - mean^2 cancels less well), then
+// GELU(LN(h)) (the erf of A&S 7.1.26, as the unfused fp16 kernel) rounded to fp16, staged and
+// stored as in linear_tile_kernel. bias, gamma and beta sit in LDS for the whole launch.
+constexpr int kLnN = 512;
+template <int KS>
+__global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16* __restrict__ gamma,
+                                                           const f16* __restrict__ beta, float eps) {
+    constexpr int MT = 128, NT = kLnN, BK = 32, NST = 3;
+    constexpr int WM = 2, WN = 4, WTN = NT / WN, NB = WTN / 32, NP = WTN / 64;
+    constexpr int SB = (MT + NT) * BK * 2;                             // 40 KiB
+    constexpr int NWP = NT * BK * 2 / 8192, NAP = MT * BK * 2 / 8192;  // 4 + 1 pieces per wave and step
+    constexpr int D = NWP + NAP;
+    constexpr int SPW = 2 * NP * 4;
+    constexpr int kPar = NST * SB;                  // vectors: bias, gamma, beta [512] fp16
+    constexpr int kRed = kPar + 3 * NT * 2;         // row partials [2][MT][WN] fp32
+    static_assert((NST - 2) * D + SPW <= 63 && KS >= NST - 1, "shape");
+    __shared__ __attribute__((aligned(16))) char smem[kRed + 2 * MT * WN * 4];
+    lds_char* const lds = (lds_char*)smem;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WM, wn = wave / WM;
+    const int r = lane & 31, hh = lane >> 5;
+    const int T = p.total, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int q8 = T >> 3, r8 = T & 7;
+    const int jb = xcd * q8 + min(xcd, r8), je = jb + q8 + (xcd < r8 ? 1 : 0);
+    const int G = ((int)gridDim.x - xcd + 7) >> 3;
+    const int j0 = jb + loc;
+    if (j0 >= je) return;
+    const int ntile_w = (je - j0 + G - 1) / G;
+    const int nsteps = ntile_w * KS;
+
+    auto src_of = [&](int t) { return tile_src<true, BK, NWP, NAP, 8>(p, (j0 + G * t) * MT, 0, wave, lane); };
+    // the vectors into LDS (loaded ahead of the first stages, written after them: the compiler's wait
+    // counts the DMA pieces), visible after the first step's barrier
+    f16x8 pv = {};
+    const f16* const pvs = tid < 64 ? p.bias : tid < 128 ? gamma : beta;
+    if (tid < 192) pv = *reinterpret_cast<const f16x8*>(pvs + (tid & 63) * 8);
+    TileSrc<NWP, NAP> cur = src_of(0);  // (the next tile's sources are computed where used: registers)
+#pragma unroll
+    for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, 8>(cur, i, smem + i * SB, wave);
+    if (tid < 192) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
+
+    auto swz = [](int row) { return (row >> 2) & 3; };
+    unsigned wro[NB], aro[2];
+    int wsw[NB], asw[2];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int wrow = wn * WTN + 32 * b + r;
+        wro[b] = (unsigned)(wrow * BK * 2), wsw[b] = swz(wrow);
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int arow = wm * 64 + 32 * b + r;
+        aro[b] = (unsigned)(NT * BK * 2 + arow * BK * 2), asw[b] = swz(arow);
+    }
+    const int cr = lane >> 3, cc = lane & 7;
+    float* const red = (float*)(void*)(smem + kRed);  // [pass][row][wn]
+    int st = 0;
+    for (int t = 0; t < ntile_w; ++t) {
+        const int m0 = (j0 + G * t) * MT;
+        const bool more = t + 1 < ntile_w;
+        f32x16 acc[NB][2] = {};
+        int st_last = 0;
+#pragma unroll 2
+        for (int ks = 0; ks < KS; ++ks) {
+            const int gs = t * KS + ks;
+            if (gs + NST - 2 > nsteps - 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            else if (ks < NST - 1 && t > 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * D + SPW) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * D) : "memory");
+            __builtin_amdgcn_s_barrier();
+            {
+                char* const fb = smem + (st == 0 ? NST - 1 : st - 1) * SB;
+                if (ks + NST - 1 < KS) tile_issue<true, BK, KS, NT, 8>(cur, ks + NST - 1, fb, wave);
+                else if (more) tile_issue<true, BK, KS, NT, 8>(src_of(t + 1), ks + NST - 1 - KS, fb, wave);
+            }
+            const unsigned sb = (unsigned)(st * SB);
+            st_last = st;
+            st = st == NST - 1 ? 0 : st + 1;
+#pragma unroll
+            for (int s = 0; s < BK / 16; ++s) {
+                const int u = 2 * s + hh;
+                f16x8 wf[NB], af[2];
+#pragma unroll
+                for (int b = 0; b < NB; ++b) wf[b] = *(lds_f16x8*)(lds + sb + wro[b] + ((u ^ wsw[b]) << 4));
+#pragma unroll
+                for (int b = 0; b < 2; ++b) af[b] = *(lds_f16x8*)(lds + sb + aro[b] + ((u ^ asw[b]) << 4));
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+                    for (int mb = 0; mb < 2; ++mb)
+                        acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[nb], af[mb], acc[nb][mb], 0, 0, 0);
+            }
+        }
+
+        // ---- epilogue: h = fp16(acc + bias) (lane: row wm*64 + 32 mb + r, 64 of the wave's channels) ----
+        const int nw0 = wn * WTN;
+        float rs[2];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            float s = 0.f;
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + (nw0 + 32 * nb + 8 * g + 4 * hh) * 2);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float h = (float)lin_val(acc[nb][mb][4 * g + u], b4[u]);
+                        acc[nb][mb][4 * g + u] = h;
+                        s += h;
+                    }
+                }
+            rs[mb] = s + __shfl_xor(s, 32, 64);  // the wave's 128 channels of the row
+        }
+        // row sums across the 4 n-waves (this tile's partials: every wave is past the last K step's
+        // reads once it reaches the barrier below, and past the previous tile's statistics reads)
+        if (hh == 0) {
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) red[(wm * 64 + 32 * mb + r) * WN + wn] = rs[mb];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        float mean[2];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const f32x4 v = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (wm * 64 + 32 * mb + r) * WN * 4);
+            mean[mb] = ((v[0] + v[1]) + (v[2] + v[3])) * (1.f / kLnN);
+            float q = 0.f;
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const float d = acc[nb][mb][e] - mean[mb];
+                    q = __builtin_fmaf(d, d, q);
+                }
+            rs[mb] = q + __shfl_xor(q, 32, 64);
+        }
+        if (hh == 0) {
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) red[MT * WN + (wm * 64 + 32 * mb + r) * WN + wn] = rs[mb];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // (also: every wave is done reading the last stage)
+        lds_char* const stg = lds + st_last * SB + wave * 4096;
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const f32x4 v = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (MT * WN + (wm * 64 + 32 * mb + r) * WN) * 4);
+            const float rstd = __builtin_amdgcn_rsqf(((v[0] + v[1]) + (v[2] + v[3])) * (1.f / kLnN) + eps);
+#pragma unroll
+            for (int np = 0; np < NP; ++np) {
+#pragma unroll
+                for (int nbl = 0; nbl < 2; ++nbl)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int n = nw0 + 64 * np + 32 * nbl + 8 * g + 4 * hh;
+                        const f16x4 g4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + NT * 2 + n * 2);
+                        const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + 2 * NT * 2 + n * 2);
+                        f16x4 o;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const float x = (acc[2 * np + nbl][mb][4 * g + u] - mean[mb]) * rstd * (float)g4[u] + (float)b4[u];
+                            o[u] = (f16)(0.5f * x * (1.f + erf_as(x * 0.70710678118654752f)));
+                        }
+                        *(__attribute__((address_space(3))) f16x4*)(stg + r * 128 + (((4 * nbl + g) ^ (r & 7)) << 4) + 8 * hh) = o;
+                    }
+                f16x8 o8[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int rl = 8 * i + cr;
+                    o8[i] = *(lds_f16x8*)(stg + rl * 128 + ((cc ^ (rl & 7)) << 4));
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = min(m0 + wm * 64 + 32 * mb + 8 * i + cr, p.m - 1);
+                    *reinterpret_cast<f16x8*>(p.out[0] + (size_t)row * NT + nw0 + 64 * np + 8 * cc) = o8[i];
+                }
+            }
+        }
+        if (more) cur = src_of(t + 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 constexpr int kTileGrid = 256;  // the 256-row forms: one workgroup per CU
+// lg_linear_cat_ln_gelu's one-launch form (linear_ln_kernel): opt-in (lg_linear_set_ln_fused). At
+// P = 16, M = 32,768 it takes 42.2 us against 25 + 17 for the two launches
+// (profiles/r05/matcher_p16_kernel_stats_ln_fused.csv): with one 128 x 512 tile per CU the ~8 k
+// cycles of GELU vector work per wave run after the GEMM, with no other wave's MFMAs beside them.
+std::atomic<int> g_ln_fused{0};
 // The tile form (tile_form below): lg_linear_set_wide(0..3) or LG_LINEAR_WIDE forces one (where n
 // allows), for tests and A/B timing; -1 (the default) chooses by size.
 std::atomic<int> g_wide{-2};
@@ -630,6 +840,37 @@ int32_t lg_linear_cat(const void* x, const void* ctx0, const void* ctx1, int32_t
     return launch<EPI_BIAS, true>(p, stream, "lg_linear_cat");
 }
 
+int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
+                              int32_t pairs, const void* w, const void* bias, const void* gamma, const void* beta,
+                              float eps, void* out, hipStream_t stream) {
+    const int k = 2 * heads * kD, m = pairs * (n0 + n1), n = k;
+    if (heads <= 0 || n0 < 0 || n1 < 0 || pairs < 0 || !shape_ok(m, n, k) || !x || !w || !bias || !gamma || !beta ||
+        !out || !aligned16(x) || (n0 && !aligned16(ctx0)) || (n1 && !aligned16(ctx1)) || !aligned16(w) ||
+        !aligned8(bias) || !aligned8(out) || !(eps >= 0.f))
+        return bad("lg_linear_cat_ln_gelu");
+    if (m == 0) return MHA_HD64_STATUS_SUCCESS;
+    const bool fused = g_ln_fused.load() && n == kLnN && (m + 127) / 128 >= 128 && aligned16(bias) && aligned16(gamma) &&
+                       aligned16(beta) && aligned16(out) && wide_mode() != 0;
+    if (!fused) {  // the projection, then LayerNorm+GELU in place (lightglue_glue.hip)
+        const int32_t st = lg_linear_cat(x, ctx0, ctx1, heads, n0, n1, pairs, w, bias, n, out, stream);
+        if (st != MHA_HD64_STATUS_SUCCESS) return st;
+        return lg_layernorm_gelu(MHA_HD64_DT_HALF, out, gamma, beta, m, n, eps, out, stream);
+    }
+    LinArgs p{};
+    p.a = (const f16*)x, p.ctx0 = (const f16*)ctx0, p.ctx1 = (const f16*)ctx1, p.w = (const f16*)w;
+    p.bias = (const f16*)bias, p.out[0] = (f16*)out;
+    p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
+    p.mtiles = (m + 127) / 128;
+    p.total = p.mtiles;
+    const int grid = p.total < kTileGrid ? p.total : kTileGrid;
+    hipLaunchKernelGGL((linear_ln_kernel<512 / 32>), dim3(grid), dim3(512), 0, stream, p, (const f16*)gamma,
+                       (const f16*)beta, eps);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
+                           : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_linear_cat_ln_gelu",
+                                                    hipGetErrorString(e));
+}
+
 int32_t lg_linear_qkv_rotary(const void* x, const void* w_perm, const void* b_perm, const void* cosv,
                              const void* sinv, int32_t heads, int32_t n0, int32_t n1, int32_t pairs, int32_t k,
                              void* q0, void* k0, void* v0, void* q1, void* k1, void* v1, hipStream_t stream) {
@@ -668,5 +909,7 @@ int32_t lg_linear_set_wide(int32_t mode) {
 }
 
 int32_t lg_glue_abi_version(void) { return LG_GLUE_ABI_VERSION; }
+
+int32_t lg_linear_set_ln_fused(int32_t on) { return g_ln_fused.exchange(on ? 1 : 0); }
 
 }  // extern "C"

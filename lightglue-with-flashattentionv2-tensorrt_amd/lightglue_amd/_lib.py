@@ -132,6 +132,7 @@ SIGNATURES.update({
     "lg_merge_heads_cat": ([_I, _P, _P, _P, _I, _I, _I, _I, _P, _P], _I),
     "lg_linear": ([_P, _P, _P, _P, _I, _I, _I, _P, _P], _I),
     "lg_linear_cat": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P, _P], _I),
+    "lg_linear_cat_ln_gelu": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, ctypes.c_float, _P, _P], _I),
     "lg_linear_qkv_rotary": ([_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P], _I),
     "lg_linear_split2": ([_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P], _I),
     "lg_layernorm_gelu": ([_I, _P, _P, _P, _I, _I, ctypes.c_float, _P, _P], _I),
@@ -139,6 +140,7 @@ SIGNATURES.update({
     "lg_log_double_softmax": ([_P, _P, _P, _I, _I, _I, _P, _P, _P], _I),
     "lg_linear_set_wide": ([_I], _I),
     "lg_glue_abi_version": ([], _I),
+    "lg_linear_set_ln_fused": ([_I], _I),
     # kernel-form switches (include/mha_hd64.h "kernel-form switches")
     "mha_hd64_set_fused_combine": ([_I], None),
     "mha_hd64_set_f32_inkernel": ([_I], None),

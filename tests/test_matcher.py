@@ -547,3 +547,47 @@ def test_wide_projections_equal_narrow(pairs, n0, n1):
             for i, (a, b) in enumerate(zip(narrow, form)):
                 for ta, tb in zip(a, b):
                     assert torch.equal(ta, tb), (f + 1, i, float((ta.float() - tb.float()).abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pairs,n0,n1", [(16, 1024, 1024), (9, 1000, 1011), (1, 700, 1301)])
+def test_linear_cat_ln_gelu_matches_torch(pairs, n0, n1):
+    """lg_linear_cat_ln_gelu (the FFN's Linear -> LayerNorm -> GELU, lightglue.py:101-106) against
+    the torch restatement on the same fp16 operands: F.linear rounded to fp16 (as the fp16 model
+    rounds h), then layer_norm and exact GELU in fp32; the default two-launch path and the opt-in
+    one-launch form (lg_linear_set_ln_fused(1): 128-row tiles owning whole rows, statistics in the
+    workgroup; 16 x 2048 and 9 x 2011 rows take it, 2001 rows stay on two launches). Bound: a few
+    fp16 ulps of the O(1) outputs."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lightglue_amd import _lib
+    from lightglue_amd import matcher as mt
+
+    F = torch.nn.functional
+    dev, dt, h = torch.device("cuda:0"), torch.float16, 4
+    lib = _lib.load()
+    gen = torch.Generator().manual_seed(5 + pairs)
+    rnd = lambda *s: torch.randn(*s, generator=gen).to(dev, dt)  # noqa: E731
+    with torch.no_grad():
+        x = rnd(1, pairs * (n0 + n1), 256) * 0.5
+        c0, c1 = rnd(pairs, h, n0, 64), rnd(pairs, h, n1, 64)
+        w, b = rnd(512, 512) * 0.05, rnd(512) * 0.1
+        ln = torch.nn.LayerNorm(512).to(dev, dt)
+        ln.weight.copy_(1 + 0.1 * rnd(512))
+        ln.bias.copy_(0.1 * rnd(512))
+        got = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)
+        prev = lib.lg_linear_set_ln_fused(1)
+        try:
+            fused = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)
+        finally:
+            lib.lg_linear_set_ln_fused(prev)
+        hh = mt._Hip.linear_cat(x, c0, c1, w, b)  # the projection alone (bits of every form)
+        ref = F.gelu(F.layer_norm(hh.float(), (512,), ln.weight.float(), ln.bias.float(), ln.eps))
+        unf = mt._Hip.layernorm_gelu(hh, ln)  # the two-launch path
+        torch.cuda.synchronize()
+    err = float((got.float() - ref).abs().max())
+    err_f = float((fused.float() - ref).abs().max())
+    print(f"cat+LN+GELU P={pairs}: max-abs {err:.3e} (one-launch form {err_f:.3e})")
+    assert torch.isfinite(got).all() and torch.isfinite(fused).all()
+    assert torch.equal(got, unf)  # the default path is the two launches
+    assert err <= 8e-3 and err_f <= 8e-3
