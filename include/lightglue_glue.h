@@ -106,6 +106,25 @@ size_t lg_log_double_softmax_workspace(int32_t m, int32_t n, int32_t batch);
 int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1, int32_t m, int32_t n, int32_t batch,
                               float* scores, void* workspace, hipStream_t stream);
 
+/* The same on the fp16 model's outputs (round 5): sim [batch, m, n] fp16 (16-B aligned, n % 8 == 0,
+ * n <= 2048) read directly, the matchability logits fp16 and strided — z0 of pair p, row i at
+ * z0[p * z_pair_stride + i * z_row_stride], z1 of pair p, column j at z1[p * z_pair_stride + j *
+ * z_row_stride] (one channel of the final projection's output) — scores fp32 (16-B aligned). Two
+ * launches; workspace >= lg_log_double_softmax_f16_workspace(m, n, batch) bytes. */
+size_t lg_log_double_softmax_f16_workspace(int32_t m, int32_t n, int32_t batch);
+int32_t lg_log_double_softmax_f16(const void* sim, const void* z0, const void* z1, int64_t z_pair_stride,
+                                  int64_t z_row_stride, int32_t m, int32_t n, int32_t batch, float* scores,
+                                  void* workspace, hipStream_t stream);
+
+/* The fp16 forward's inputs (lightglue.py:329-337 and FourierPositionalEncoding :32-52), round 5:
+ * x [pairs * (n0 + n1), dim] pair-major from desc0 [pairs, n0, dim] and desc1 [pairs, n1, dim]
+ * (dim = 256, 16-B aligned), and the rotary tables cos, sin [pairs * (n0 + n1), 64] from kpts0
+ * [pairs, n0, 2], kpts1 [pairs, n1, 2] and Wr [32, 2] (all fp16): proj = Wr · kpt rounded to fp16,
+ * cos / sin of it rounded to fp16, each value repeated for the two members of a rotary pair. */
+int32_t lg_pair_inputs(const void* desc0, const void* desc1, const void* kpts0, const void* kpts1, const void* wr,
+                       int32_t n0, int32_t n1, int32_t pairs, int32_t dim, void* x, void* cosv, void* sinv,
+                       hipStream_t stream);
+
 /* Test and benchmark hook: the projections' tile forms for launches of many rows (several image
  * pairs per forward): 0 the 64 x 64 form only, 1 the 256 x 128 form where n allows, 2 the
  * 256 x 256 form where n allows, 3 the 256 x 256 form with a fifth ring stage (A/B only), -1 (the

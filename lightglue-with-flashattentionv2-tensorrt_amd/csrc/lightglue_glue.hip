@@ -312,6 +312,215 @@ __global__ __launch_bounds__(256) void dual_combine_kernel(const float* __restri
         out[(size_t)i * n + j] = 2.f * sim[(size_t)i * n + j] - lse_row[i] - cterm + log_sigmoid(z0[i]) + zj;
 }
 
+// ---- dual log-softmax on the fp16 similarity (round 5; the fp16 matcher's assignment head) ----
+// The fp16 model computes sim = m0·m1ᵀ in fp16 and the reference takes .float() of it
+// (lightglue.py:214-216); these kernels read the fp16 sim and the fp16 matchability logits (strided:
+// one channel of the final projection's output) directly, so no fp32 copies exist. Pass 1: a block
+// is 64 rows x all columns of one pair; each of its 8 waves loads a batch of 8 rows at once (a lane
+// owns 16 columns, 16-B loads): the row logsumexp of each (wave max, then the exp sum) and, per
+// column, the batch's max and one exponential per element into a running (max, sum), merged over
+// the 8 waves through LDS into one partial per (64-row block, column). (Round 5: 115 -> 49.6 us at
+// P = 16 against the fp32 kernels above on a .float() copy, profiles/r05/matcher_p16_kernel_stats_head.csv.)
+// Pass 2: a block is 64 rows; it first closes the column logsumexp (+ log-sigmoid of z1) of every
+// column from the partials into LDS, then writes its rows as fp32 with 16-B stores.
+constexpr int kDsRows = 64;  // rows per block, both passes
+
+struct DsArgs {
+    const f16* sim;            // [batch, m, n]
+    const f16* z0;             // row i of pair p at z0[p * zps + i * zrs]
+    const f16* z1;             // column j of pair p at z1[p * zps + j * zrs]
+    long zps, zrs;
+    float* scores;             // [batch, m, n]
+    float* lse_row;            // workspace: [batch][m]
+    float2* col_part;          // workspace: [batch][m / 64][n]
+    int m, n, rblocks;
+};
+
+__device__ __forceinline__ void lse_step(float& mx, float& s, float v) {  // online (max, sum) of exp
+    if (v > mx) {
+        s = s * __expf(mx - v) + 1.f;
+        mx = v;
+    } else {
+        s += __expf(v - mx);
+    }
+}
+
+constexpr int kDsBatch = 8;  // rows a wave loads at once (16 KiB in flight per wave at n = 1024)
+constexpr int kDsWaves = 8;  // waves per block: kDsRows / kDsWaves = one batch of rows each
+
+template <int CPL>  // columns per lane in units of 8 (n <= 512 CPL)
+__global__ __launch_bounds__(64 * kDsWaves) void lse16_kernel(DsArgs a) {
+    typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+    const int p = blockIdx.y, rb = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const f16* sim = a.sim + (size_t)p * a.m * a.n;
+    float cm[CPL][8], cs[CPL][8];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cm[c][e] = -INFINITY, cs[c][e] = 0.f;
+    const int r0 = rb * kDsRows + wave * (kDsRows / kDsWaves);
+    const int r1 = min(r0 + kDsRows / kDsWaves, a.m);
+    for (int i0 = r0; i0 < r1; i0 += kDsBatch) {
+        // a batch of rows, every load issued first (rows past the block's end: -inf)
+        f16x8 x[kDsBatch][CPL];
+#pragma unroll
+        for (int b = 0; b < kDsBatch; ++b)
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int j = (c * 64 + lane) * 8;
+                if (i0 + b < r1 && j < a.n) x[b][c] = *reinterpret_cast<const f16x8*>(sim + (size_t)(i0 + b) * a.n + j);
+                else
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) x[b][c][e] = (f16)-INFINITY;
+            }
+        // row logsumexp of each row of the batch (independent wave reductions)
+        float mx[kDsBatch], s[kDsBatch];
+#pragma unroll
+        for (int b = 0; b < kDsBatch; ++b) {
+            mx[b] = -INFINITY;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) mx[b] = fmaxf(mx[b], (float)x[b][c][e]);
+        }
+#pragma unroll
+        for (int b = 0; b < kDsBatch; ++b) mx[b] = wave_max(mx[b]);
+#pragma unroll
+        for (int b = 0; b < kDsBatch; ++b) {
+            s[b] = 0.f;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) s[b] += __expf((float)x[b][c][e] - mx[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < kDsBatch; ++b) s[b] = wave_sum(s[b]);
+        if (lane < kDsBatch) {
+            float l = 0.f;
+#pragma unroll
+            for (int b = 0; b < kDsBatch; ++b)
+                if (lane == b) l = mx[b] + __logf(s[b]);
+            if (i0 + lane < r1) a.lse_row[(size_t)p * a.m + i0 + lane] = l;
+        }
+        // per column: the batch's max, then one exponential per element
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float bm = (float)x[0][c][e];
+#pragma unroll
+                for (int b = 1; b < kDsBatch; ++b) bm = fmaxf(bm, (float)x[b][c][e]);
+                const float nm = fmaxf(cm[c][e], bm);
+                if (nm == -INFINITY) continue;  // (columns past n)
+                float t = cs[c][e] * __expf(cm[c][e] - nm);
+#pragma unroll
+                for (int b = 0; b < kDsBatch; ++b) t += __expf((float)x[b][c][e] - nm);
+                cm[c][e] = nm, cs[c][e] = t;
+            }
+    }
+    // the waves' column partials -> one per (block, column)
+    __shared__ float2 part[kDsWaves][64 * 8];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) part[wave][lane * 8 + e] = make_float2(cm[c][e], cs[c][e]);
+        __syncthreads();
+        for (int t = threadIdx.x; t < 512; t += 64 * kDsWaves) {
+            const int j = c * 512 + t;
+            float mx = part[0][t].x, s = part[0][t].y;
+#pragma unroll
+            for (int w = 1; w < kDsWaves; ++w) lse_merge(mx, s, part[w][t].x, part[w][t].y);
+            if (j < a.n) a.col_part[((size_t)p * a.rblocks + rb) * a.n + j] = make_float2(mx, s);
+        }
+        __syncthreads();
+    }
+}
+
+template <int CPL>
+__global__ __launch_bounds__(64 * kDsWaves) void combine16_kernel(DsArgs a) {
+    typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const int p = blockIdx.y, rb = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ float cterm[512 * CPL];  // logsig(z1[j]) - lse_col[j]
+    for (int j = threadIdx.x; j < a.n; j += 64 * kDsWaves) {
+        float2 q[16];
+        float mx = -INFINITY, s = 0.f;
+        for (int b0 = 0; b0 < a.rblocks; b0 += 16) {  // (16 partial loads in flight)
+#pragma unroll
+            for (int b = 0; b < 16; ++b)
+                q[b] = b0 + b < a.rblocks ? a.col_part[((size_t)p * a.rblocks + b0 + b) * a.n + j] : make_float2(-INFINITY, 0.f);
+#pragma unroll
+            for (int b = 0; b < 16; ++b) lse_merge(mx, s, q[b].x, q[b].y);
+        }
+        cterm[j] = log_sigmoid((float)a.z1[p * a.zps + j * a.zrs]) - (logf(s) + mx);
+    }
+    __syncthreads();
+    const f16* sim = a.sim + (size_t)p * a.m * a.n;
+    float* out = a.scores + (size_t)p * a.m * a.n;
+    const int r0 = rb * kDsRows + wave * (kDsRows / kDsWaves);
+    const int r1 = min(r0 + kDsRows / kDsWaves, a.m);
+    for (int i0 = r0; i0 < r1; i0 += kDsBatch) {
+        f16x8 x[kDsBatch][CPL];
+        float rterm[kDsBatch];
+#pragma unroll
+        for (int b = 0; b < kDsBatch; ++b) {
+            const int i = min(i0 + b, r1 - 1);
+            rterm[b] = log_sigmoid((float)a.z0[p * a.zps + (long)i * a.zrs]) - a.lse_row[(size_t)p * a.m + i];
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int j = (c * 64 + lane) * 8;
+                if (j < a.n) x[b][c] = *reinterpret_cast<const f16x8*>(sim + (size_t)i * a.n + j);
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < kDsBatch; ++b) {
+            if (i0 + b >= r1) break;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int j = (c * 64 + lane) * 8;
+                if (j >= a.n) continue;
+                f32x4 o0, o1;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    o0[e] = 2.f * (float)x[b][c][e] + rterm[b] + cterm[j + e];
+                    o1[e] = 2.f * (float)x[b][c][e + 4] + rterm[b] + cterm[j + e + 4];
+                }
+                *reinterpret_cast<f32x4*>(out + (size_t)(i0 + b) * a.n + j) = o0;
+                *reinterpret_cast<f32x4*>(out + (size_t)(i0 + b) * a.n + j + 4) = o1;
+            }
+        }
+    }
+}
+
+// ---- the forward's inputs in the pair-major layout + the positional encoding (round 5) ----
+// x [pairs * (n0 + n1), dim] from desc0 [pairs, n0, dim], desc1 [pairs, n1, dim] (the reference's
+// torch.cat of the two images, lightglue.py:332-336, pairs stacked), and the rotary tables cos, sin
+// [rows, 64] of FourierPositionalEncoding (lightglue.py:32-52): proj_k = Wr[k] · kpt rounded to fp16
+// (the fp16 model's Linear(2, 32)), cos / sin of it rounded to fp16, each repeated for the two
+// members of a rotary pair. A block is 8 rows; per row 32 threads copy the descriptor (16 B each,
+// dim = 256) and compute one (cos, sin) pair each.
+__global__ __launch_bounds__(256) void pair_inputs_kernel(const f16* __restrict__ d0, const f16* __restrict__ d1,
+                                                          const f16* __restrict__ k0, const f16* __restrict__ k1,
+                                                          const f16* __restrict__ wr, int n0, int n1, int rows,
+                                                          f16* x, f16* cosv, f16* sinv) {
+    typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+    typedef f16 f16x2 __attribute__((ext_vector_type(2)));
+    const int row = blockIdx.x * 8 + (threadIdx.x >> 5), t = threadIdx.x & 31;
+    if (row >= rows) return;
+    const int ntot = n0 + n1, p = row / ntot, l = row - p * ntot;
+    const bool first = l < n0;
+    const size_t src = first ? (size_t)p * n0 + l : (size_t)p * n1 + (l - n0);
+    const f16* d = first ? d0 : d1;
+    const f16* kp = (first ? k0 : k1) + src * 2;
+    *reinterpret_cast<f16x8*>(x + (size_t)row * 256 + t * 8) = *reinterpret_cast<const f16x8*>(d + src * 256 + t * 8);
+    const float proj = (float)(f16)((float)wr[2 * t] * (float)kp[0] + (float)wr[2 * t + 1] * (float)kp[1]);
+    const f16 c = (f16)cosf(proj), s = (f16)sinf(proj);
+    *reinterpret_cast<f16x2*>(cosv + (size_t)row * kD + 2 * t) = f16x2{c, c};
+    *reinterpret_cast<f16x2*>(sinv + (size_t)row * kD + 2 * t) = f16x2{s, s};
+}
+
 inline unsigned blocks_for(long threads) { return (unsigned)((threads + 255) / 256); }
 
 int32_t launched(const char* what) {
@@ -467,6 +676,58 @@ int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1
     hipLaunchKernelGGL(dual_combine_kernel, dim3(((m + kCombRows - 1) / kCombRows) * ((n + 255) / 256), batch),
                        dim3(256), 0, stream, sim, z0, z1, lse_row, col_part, chunks, m, n, scores, ws_stride);
     return launched("lg_log_double_softmax");
+}
+
+size_t lg_log_double_softmax_f16_workspace(int32_t m, int32_t n, int32_t batch) {
+    if (m <= 0 || n <= 0 || batch <= 0) return 0;
+    const size_t rb = (size_t)(m + kDsRows - 1) / kDsRows;
+    return ((size_t)batch * m * sizeof(float) + 255) / 256 * 256 + (size_t)batch * rb * n * sizeof(float2);
+}
+
+int32_t lg_log_double_softmax_f16(const void* sim, const void* z0, const void* z1, int64_t z_pair_stride,
+                                  int64_t z_row_stride, int32_t m, int32_t n, int32_t batch, float* scores,
+                                  void* workspace, hipStream_t stream) {
+    if (m < 0 || n < 0 || batch < 0 || n % 8 != 0 || n > 2048 ||
+        ((m > 0 && n > 0 && batch > 0) &&
+         (!sim || !z0 || !z1 || !scores || !workspace || (reinterpret_cast<uintptr_t>(sim) & 15) ||
+          (reinterpret_cast<uintptr_t>(scores) & 15))))
+        return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_log_double_softmax_f16", "bad arguments");
+    if (m == 0 || n == 0 || batch == 0) return MHA_HD64_STATUS_SUCCESS;
+    DsArgs a;
+    a.sim = (const f16*)sim, a.z0 = (const f16*)z0, a.z1 = (const f16*)z1, a.zps = z_pair_stride, a.zrs = z_row_stride;
+    a.scores = scores, a.m = m, a.n = n, a.rblocks = (m + kDsRows - 1) / kDsRows;
+    a.lse_row = reinterpret_cast<float*>(workspace);
+    a.col_part = reinterpret_cast<float2*>(reinterpret_cast<char*>(workspace) +
+                                           ((size_t)batch * m * sizeof(float) + 255) / 256 * 256);
+    const dim3 grid(a.rblocks, batch);
+#define LG_DS(CPL)                                                                        \
+    hipLaunchKernelGGL((lse16_kernel<CPL>), grid, dim3(64 * kDsWaves), 0, stream, a);     \
+    hipLaunchKernelGGL((combine16_kernel<CPL>), grid, dim3(64 * kDsWaves), 0, stream, a);
+    if (n <= 512) {
+        LG_DS(1)
+    } else if (n <= 1024) {
+        LG_DS(2)
+    } else {
+        LG_DS(4)
+    }
+#undef LG_DS
+    return launched("lg_log_double_softmax_f16");
+}
+
+int32_t lg_pair_inputs(const void* desc0, const void* desc1, const void* kpts0, const void* kpts1, const void* wr,
+                       int32_t n0, int32_t n1, int32_t pairs, int32_t dim, void* x, void* cosv, void* sinv,
+                       hipStream_t stream) {
+    const long rows = (long)pairs * (n0 + n1);
+    if (n0 < 0 || n1 < 0 || pairs < 0 || dim != 256 || (rows > 0 && (!x || !cosv || !sinv || !wr)) ||
+        (n0 > 0 && (!desc0 || !kpts0)) || (n1 > 0 && (!desc1 || !kpts1)) ||
+        ((reinterpret_cast<uintptr_t>(desc0) | reinterpret_cast<uintptr_t>(desc1) | reinterpret_cast<uintptr_t>(x)) & 15) ||
+        ((reinterpret_cast<uintptr_t>(cosv) | reinterpret_cast<uintptr_t>(sinv)) & 3) || rows > (1L << 30))
+        return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, "lg_pair_inputs", "bad arguments");
+    if (rows == 0) return MHA_HD64_STATUS_SUCCESS;
+    hipLaunchKernelGGL(pair_inputs_kernel, dim3((unsigned)((rows + 7) / 8)), dim3(256), 0, stream, (const f16*)desc0,
+                       (const f16*)desc1, (const f16*)kpts0, (const f16*)kpts1, (const f16*)wr, n0, n1, (int)rows,
+                       (f16*)x, (f16*)cosv, (f16*)sinv);
+    return launched("lg_pair_inputs");
 }
 
 }  // extern "C"

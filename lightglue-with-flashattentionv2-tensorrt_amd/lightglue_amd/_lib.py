@@ -140,6 +140,9 @@ SIGNATURES.update({
     "lg_log_double_softmax": ([_P, _P, _P, _I, _I, _I, _P, _P, _P], _I),
     "lg_linear_set_wide": ([_I], _I),
     "lg_glue_abi_version": ([], _I),
+    "lg_log_double_softmax_f16_workspace": ([_I, _I, _I], _S),
+    "lg_log_double_softmax_f16": ([_P, _P, _P, ctypes.c_int64, ctypes.c_int64, _I, _I, _I, _P, _P, _P], _I),
+    "lg_pair_inputs": ([_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P], _I),
     "lg_linear_set_ln_fused": ([_I], _I),
     # kernel-form switches (include/mha_hd64.h "kernel-form switches")
     "mha_hd64_set_fused_combine": ([_I], None),

@@ -186,6 +186,36 @@ class _Hip:
         return out
 
 
+    @staticmethod
+    def log_double_softmax_f16(sim, v, m, zc):
+        """sim [P, m, n] fp16 (contiguous); the matchability logits at channel zc of v [P, m + n, C]
+        (the assignment projection's output): one fp32 scores tensor [P, m, n], two launches."""
+        pr, n, ch = sim.shape[0], sim.shape[2], v.shape[2]
+        lib = _lib.load()
+        out = torch.empty(sim.shape, dtype=torch.float32, device=sim.device)
+        stream = _Hip._stream(sim)
+        ws = _workspace(sim.device, stream, lib.lg_log_double_softmax_f16_workspace(m, n, pr))
+        base = v.data_ptr() + zc * v.element_size()
+        st = lib.lg_log_double_softmax_f16(sim.data_ptr(), base, base + m * ch * v.element_size(), (m + n) * ch, ch,
+                                           m, n, pr, out.data_ptr(), ws.data_ptr(), stream)
+        _check(st, "lg_log_double_softmax_f16")
+        return out
+
+    @staticmethod
+    def pair_inputs(desc0, desc1, kpts0, kpts1, wr):
+        """x [1, P*(m+n), 256] pair-major and the rotary tables cos, sin [1, P*(m+n), 64] in one launch."""
+        pr, m, n, d = desc0.shape[0], desc0.shape[1], desc1.shape[1], desc0.shape[2]
+        rows = pr * (m + n)
+        x = torch.empty((1, rows, d), dtype=desc0.dtype, device=desc0.device)
+        cos = torch.empty((1, rows, 64), dtype=desc0.dtype, device=desc0.device)
+        sin = torch.empty_like(cos)
+        t = [u.contiguous() for u in (desc0, desc1, kpts0, kpts1, wr)]
+        st = _lib.load().lg_pair_inputs(*(u.data_ptr() for u in t), m, n, pr, d, x.data_ptr(), cos.data_ptr(),
+                                        sin.data_ptr(), _Hip._stream(desc0))
+        _check(st, "lg_pair_inputs")
+        return x, cos, sin
+
+
 def _cached(module: nn.Module, name: str, params: Sequence[torch.Tensor], dtype: torch.dtype, build):
     """Derived weights cached on `module`, rebuilt when any source parameter changes (in-place
     updates bump ``_version``; load_state_dict does) or the dtype/device differs."""
@@ -407,6 +437,30 @@ class MatchAssignment(nn.Module):
         self.final_proj = nn.Linear(d, d)
         self.matchability = nn.Linear(d, 1)
 
+    def hip16_ok(self, x: torch.Tensor, n: int) -> bool:
+        return x.dtype == torch.float16 and x.is_cuda and x.shape[-1] == 256 and n % 8 == 0 and n <= 2048
+
+    def forward_rows(self, x: torch.Tensor, pr: int, m: int, n: int) -> torch.Tensor:
+        """fp16 hip path on both images' rows x [1, P*(m+n), d] at once: ONE projection with
+        [W_final / scale ; w_match ; 0] (d^0.25 = 4 for d = 256: the scaling is exact in fp16, so
+        this equals fp16(final_proj(d)) / scale), the similarity as one batched GEMM on the fp16
+        halves, and the dual log-softmax reading the fp16 similarity and the matchability channel
+        directly (lightglue.py:208-233)."""
+        d = x.shape[-1]
+        fp, mt = self.final_proj, self.matchability
+
+        def build():
+            w = torch.zeros((384, d), dtype=torch.float32, device=x.device)
+            b = torch.zeros((384,), dtype=torch.float32, device=x.device)
+            w[:d], b[:d] = fp.weight.float() / self.scale, fp.bias.float() / self.scale
+            w[d], b[d] = mt.weight.float()[0], mt.bias.float()[0]
+            return w, b
+
+        w, b = _cached(self, "_assign_aug", (fp.weight, fp.bias, mt.weight, mt.bias), x.dtype, build)
+        v = _Hip.linear(x, w, b).view(pr, m + n, 384)
+        sim = torch.bmm(v[:, :m, :d], v[:, m:, :d].transpose(1, 2))   # fp16 [P, m, n]
+        return _Hip.log_double_softmax_f16(sim, v, m, d)
+
     def forward(self, d0: torch.Tensor, d1: torch.Tensor, hip: bool = False) -> torch.Tensor:
         m0 = self.final_proj(d0) / self.scale
         m1 = self.final_proj(d1) / self.scale
@@ -462,20 +516,27 @@ class LightGlueMatcher(nn.Module):
             outs = [self.forward(kpts0[i:i + 1], kpts1[i:i + 1], desc0[i:i + 1], desc1[i:i + 1]) for i in range(pr)]
             return tuple(torch.cat(t, 0) for t in zip(*outs))
         splits = (m, n, pr)
-        x = self.input_proj(torch.cat((desc0, desc1), 1))          # [P, M+N, d], pair-major rows
-        if hip and not x.is_cuda:
-            raise PluginError("LightGlueMatcher(glue='hip') runs on the GPU only (no CPU fallback)")
-        cos, sin = self.posenc(torch.cat((kpts0, kpts1), 1).to(x.dtype))
         rows = pr * (m + n)
-        x = x.reshape(1, rows, x.shape[-1])
-        cos, sin = cos.reshape(1, rows, -1), sin.reshape(1, rows, -1)  # [1, P*(M+N), 64], broadcast over heads
-        if hip:
-            cos, sin = cos.contiguous(), sin.contiguous()
+        if hip and not desc0.is_cuda:
+            raise PluginError("LightGlueMatcher(glue='hip') runs on the GPU only (no CPU fallback)")
+        fast = hip and desc0.dtype == torch.float16 and isinstance(self.input_proj, nn.Identity) and \
+            desc0.shape[-1] == 256 and kpts0.dtype == torch.float16
+        if fast:  # pair-major rows and the positional encoding in one launch
+            x, cos, sin = _Hip.pair_inputs(desc0, desc1, kpts0, kpts1, self.posenc.Wr.weight)
+        else:
+            x = self.input_proj(torch.cat((desc0, desc1), 1))          # [P, M+N, d], pair-major rows
+            cos, sin = self.posenc(torch.cat((kpts0, kpts1), 1).to(x.dtype))
+            x = x.reshape(1, rows, x.shape[-1])
+            cos, sin = cos.reshape(1, rows, -1), sin.reshape(1, rows, -1)  # [1, P*(M+N), 64], broadcast over heads
+            if hip:
+                cos, sin = cos.contiguous(), sin.contiguous()
         for layer in self.transformers:
             x = layer(x, cos, sin, splits, self.attention, hip)
+        head = self.log_assignment[self.n_layers - 1]
+        scores = head.forward_rows(x, pr, m, n) if hip and head.hip16_ok(x, n) else None
         x = x.view(pr, m + n, x.shape[-1])
         d0, d1 = x[:, :m], x[:, m:]
-        return d0, d1, self.log_assignment[self.n_layers - 1](d0, d1, hip)
+        return d0, d1, scores if scores is not None else head(d0, d1, hip)
 
     def match(self, kpts0, kpts1, desc0, desc1):
         """forward + filter_matches (the demo's post-processing); for P > 1 pairs a list of

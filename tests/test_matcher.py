@@ -591,3 +591,38 @@ def test_linear_cat_ln_gelu_matches_torch(pairs, n0, n1):
     assert torch.isfinite(got).all() and torch.isfinite(fused).all()
     assert torch.equal(got, unf)  # the default path is the two launches
     assert err <= 8e-3 and err_f <= 8e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pairs,m,n", [(1, 64, 48), (3, 300, 256), (1, 130, 211), (16, 1024, 1024), (2, 2048, 2000)])
+def test_fp16_head_and_inputs_kernels(pairs, m, n):
+    """The fp16 forward's own kernels around the layers: lg_pair_inputs (pair-major x = the torch cat
+    bit for bit; cos / sin = the fp16 FourierPositionalEncoding within one fp16 ulp) and
+    lg_log_double_softmax_f16 (fp16 sim and strided fp16 matchability logits read directly) against
+    the torch restatement of lightglue.py:197-205 on the same fp16 inputs."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lightglue_amd import matcher as mt
+
+    dev, dt = torch.device("cuda:0"), torch.float16
+    gen = torch.Generator().manual_seed(pairs * 7 + m)
+    rnd = lambda *s: torch.randn(*s, generator=gen).to(dev, dt)  # noqa: E731
+    with torch.no_grad():
+        d0, d1 = rnd(pairs, m, 256), rnd(pairs, n, 256)
+        k0, k1 = rnd(pairs, m, 2), rnd(pairs, n, 2)
+        pe = mt.FourierPositionalEncoding(2, 64).to(dev, dt)
+        x, cos, sin = mt._Hip.pair_inputs(d0, d1, k0, k1, pe.Wr.weight)
+        rc, rs = pe(torch.cat((k0, k1), 1))
+        assert torch.equal(x.view(pairs, m + n, 256), torch.cat((d0, d1), 1))
+        for got, ref in ((cos, rc), (sin, rs)):
+            assert float((got.view(pairs, m + n, 64).float() - ref.reshape(pairs, m + n, 64).float()).abs().max()) <= 1e-3
+        if n % 8:
+            return
+        v = rnd(pairs, m + n, 384) * 2
+        sim = rnd(pairs, m, n) * 4
+        got = mt._Hip.log_double_softmax_f16(sim, v, m, 256)
+        ref = mt.log_double_softmax(sim.float(), v[:, :m, 256:257].float(), v[:, m:, 256:257].float())
+        torch.cuda.synchronize()
+    err = float((got - ref).abs().max())
+    print(f"dual log-softmax f16 P={pairs} {m}x{n}: max-abs {err:.3e}")
+    assert err <= 2e-4 * max(1.0, float(ref.abs().max()) / 16)

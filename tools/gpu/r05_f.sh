@@ -1,10 +1,10 @@
 #!/bin/bash
 # round 5, call F: FFN input projection with LayerNorm + GELU in its epilogue
 set -o pipefail
-O=$PWD/gpurun_out/r05g; mkdir -p $O
+O=$PWD/gpurun_out/r05j; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_matcher.py -x -q -s -m gpu --timeout 150 --timeout-method thread > $O/matcher_tests.log 2>&1 || exit 1
 timeout -k 10 150 python tools/matcher_profile.py 16 1024 20 > $O/mprof.txt 2>&1 || exit 1
-timeout -k 10 150 python tools/linear_ab.py 16 1024 "" 1 b > $O/linear_ab.jsonl 2>&1 || exit 1
+timeout -k 10 150 python tools/matcher_profile.py 8 1024 20 >> $O/mprof.txt 2>&1 || exit 1
 timeout -k 10 150 python tools/matcher_profile.py 32 1024 10 >> $O/mprof.txt 2>&1 || exit 1
 R=$PWD
 cd /tmp && export TMPDIR=/tmp
