@@ -365,6 +365,37 @@ def test_dma_hazard_rules_on_synthetic_sequences():
     assert c.check(seq(("s_mov_b32", "m0", " s3"), ("s_nop", "0", ""), load)) == (1, 0)
     assert c.check(seq(("v_readfirstlane_b32", "s3", " v2"), ("s_mov_b32", "m0", " s3"), ("s_nop", "0", ""), load)) == (1, 0)
 
+    # branch targets: the walk stops at an instruction another block jumps to, and
+    # counts it unless the load already has its 5 wait states after the target
+    def seq_t(targets, *ins):
+        return [("k", [(op, dst, src) for op, dst, src in ins], set(targets))]
+
+    body = (("s_add_i32", "s6", " s6, 1"), ("s_nop", "0", ""), load)
+    assert c.check(seq_t((), *body)) == (1, 0)  # straight line: fine
+    assert c.check(seq_t((1,), *body)) == (1, 1)  # s_nop 0 is a jump target: 1 wait state only
+    assert c.check(seq_t((0,), ("s_nop", "4", ""), load)) == (1, 0)  # padded after the target
+    assert c.check(seq_t((2,), ("v_readfirstlane_b32", "s4", " v2"), ("s_nop", "4", ""), load)) == (1, 1)
+
+
+def test_dma_hazard_parser_finds_branch_targets():
+    """parse() maps an s_cbranch's `<func+0x..>` target to the instruction at that address."""
+    c = _dma_checker()
+    lines = [
+        "0000000000001000 <k>:",
+        "\ts_mov_b32 s4, 0  // 000000001000: BEEF0000",
+        "\ts_cbranch_scc1 1  // 000000001004: BF850001 <k+0x10>",
+        "\tv_readfirstlane_b32 s4, v2  // 00000000100C: 7E080502",
+        "\ts_nop 0  // 000000001010: BF800000",
+        "\tbuffer_load_dwordx4 v1, s[8:11], s4 offen lds  // 000000001014: E05D1000 02020001",
+    ]
+    funcs = c.parse(lines)
+    assert funcs[0][0] == "k" and funcs[0][2] == {3}
+    # the load sits 1 wait state after a jump target: flagged there (the walk stops at it)
+    assert c.check(funcs) == (1, 1)
+    # without the branch, the same code is flagged for the VALU write of s4 one wait state away
+    assert c.check([(funcs[0][0], funcs[0][1], set())]) == (1, 1)
+    assert c.check([(funcs[0][0], funcs[0][1][3:], set())]) == (1, 0)
+
 
 def test_built_library_dma_wait_states():
     """Every LDS-DMA load of the built gfx950 code objects keeps the wait states (inline asm: the

@@ -6,7 +6,10 @@ before it (straight-line, in emission order) and check:
   * a VALU instruction that writes an SGPR the load reads (its descriptor, its soffset, M0) needs
     5 wait states before the load;
   * a SALU write of M0 needs 1 wait state before an LDS-DMA load.
-Wait states: every instruction counts 1, `s_nop N` counts N + 1.
+Wait states: every instruction counts 1, `s_nop N` counts N + 1. The walk follows one path only,
+so it stops at a branch target (an instruction some s_branch / s_cbranch jumps to: its other
+predecessors are not walked) and counts that as a violation unless the 5 wait states are already
+in place between the target and the load.
 
     python tools/check_dma_hazards.py [lib/libmha_hd64.so]
 Exit status 1 on a violation. Needs objcopy, clang-offload-bundler and llvm-objdump (ROCm).
@@ -60,32 +63,44 @@ def sgprs(text):
 
 
 def parse(lines):
-    """-> list of (function, [(op, dst_text, src_text)])"""
-    funcs, cur, name = [], [], None
+    """-> list of (function, [(op, dst_text, src_text)], {indices of branch targets})"""
+    funcs, cur, addrs, tgts, name, start = [], [], [], [], None, 0
+
+    def close():
+        if name is not None:
+            at = {a: k for k, a in enumerate(addrs)}
+            funcs.append((name, cur, {at[t] for t in tgts if t in at}))
+
     for raw in lines:
-        m = re.match(r"^[0-9a-f]+ <(.+)>:", raw)
+        m = re.match(r"^([0-9a-f]+) <(.+)>:", raw)
         if m:
-            if name is not None:
-                funcs.append((name, cur))
-            name, cur = m.group(1), []
+            close()
+            name, start, cur, addrs, tgts = m.group(2), int(m.group(1), 16), [], [], []
             continue
         s = raw.strip()
         if not s or s.startswith(";") or s.endswith(">:") or ":" in s.split()[0]:
             continue
-        s = s.split("//")[0].strip()
-        parts = s.split(None, 1)
+        code, _, comment = s.partition("//")
+        a = re.match(r"\s*([0-9A-Fa-f]+):", comment)
+        parts = code.strip().split(None, 1)
         op = parts[0]
         args = parts[1] if len(parts) > 1 else ""
         dst, _, src = args.partition(",")
         cur.append((op, dst.strip(), src))
-    if name is not None:
-        funcs.append((name, cur))
+        addrs.append(int(a.group(1), 16) if a else -1)
+        t = re.search(r"<[^>+]+\+(0x[0-9a-f]+)>", comment)
+        if op.startswith(("s_branch", "s_cbranch")) and t:
+            tgts.append(start + int(t.group(1), 16))
+    close()
     return funcs
 
 
 def check(funcs):
+    """funcs: (name, instructions[, branch-target indices]) -> (LDS-DMA loads checked, violations)"""
     bad = checked = 0
-    for name, ins in funcs:
+    for f in funcs:
+        name, ins = f[0], f[1]
+        targets = f[2] if len(f) > 2 else set()
         for i, (op, dst, src) in enumerate(ins):
             if not (op.startswith("buffer_load_dword") and " lds" in (dst + "," + src) + " "):
                 if not (op.startswith("buffer_load_dword") and src.rstrip().endswith("lds")):
@@ -93,10 +108,16 @@ def check(funcs):
             checked += 1
             reads = sgprs(src) | {"m0"}
             ws = 0  # wait states between instruction j and the load
-            for j in range(i - 1, max(-1, i - 12), -1):
+            k = i  # the walk has covered ins[k .. i - 1]
+            while k > 0 and ws < 5:
+                if k in targets:  # other predecessors jump here: not walked
+                    print(f"{name}: branch target {ws} wait states before '{op}' (predecessors not checked)")
+                    bad += 1
+                    break
+                j = k - 1
                 pop, pdst, _ = ins[j]
                 written = sgprs(pdst) if not pop.startswith(("s_nop", "s_waitcnt", "s_barrier", "buffer_", "ds_", "s_cbranch", "s_branch")) else set()
-                if pop.startswith("v_") and written & reads and ws < 5:
+                if pop.startswith("v_") and written & reads:
                     print(f"{name}: VALU '{pop} {pdst}' writes {sorted(written & reads)} {ws} wait states before '{op}'")
                     bad += 1
                 if pop.startswith("s_") and "m0" in written and ws < 1:
@@ -107,8 +128,7 @@ def check(funcs):
                     ws += (int(m.group(1), 0) if m else 0) + 1
                 else:
                     ws += 1
-                if ws >= 5:
-                    break
+                k = j
     return checked, bad
 
 

@@ -14,7 +14,9 @@ from collections import defaultdict
 
 
 def short(name):
-    return name.split("(")[0].replace("mha_hd64::(anonymous namespace)::", "")
+    # drop the return type and the namespaces that carry parentheses, then the argument list
+    name = name.removeprefix("void ").replace("(anonymous namespace)::", "").replace("mha_hd64::", "")
+    return name.split("(")[0]
 
 
 def main():
