@@ -216,6 +216,87 @@ __global__ __launch_bounds__(256) void ln_gelu_512_f16_kernel(const f16* __restr
     *reinterpret_cast<f16x8*>(y + (size_t)row * 512 + lane * 8) = o;
 }
 
+// A/B build only (SRC=glue tools/build_linear_variant.sh <name> -DLG_LN_FORM=1, tools/ln_ab.py): the
+// same operator, persistent: wave w of W walks rows w, w + W, ... with the loads of its next DEPTH
+// rows in flight while it computes one, gamma / beta converted once per wave, and GELU as
+// max(t, 0) - |t| * (y / 2) * exp(-t^2 / 2) (the same A&S 7.1.26 terms as erf_as, folded: for t >= 0
+// t * Phi(t) = t - t * (y e / 2), for t < 0 it is -|t| * (y e / 2); no 1 + erf cancellation).
+// Measured no faster (16.9-19.2 vs 17.0 us at 32,768 rows, profiles/r05/ln_gelu_persistent_ab.jsonl):
+// the per-row kernel is vector-issue bound, not latency bound.
+#ifndef LG_LN_FORM
+#define LG_LN_FORM 0
+#endif
+#if LG_LN_FORM == 1
+#ifndef LG_LN_DEPTH
+#define LG_LN_DEPTH 2
+#endif
+#ifndef LG_LN_BPC
+#define LG_LN_BPC 4
+#endif
+constexpr int kLnDepth = LG_LN_DEPTH;  // rows in flight per wave beyond the one computed
+constexpr int kLnBlocksPerCU = LG_LN_BPC;
+__global__ __launch_bounds__(256) void ln_gelu_512_rows_kernel(const f16* __restrict__ x, const f16* __restrict__ g,
+                                                               const f16* __restrict__ bta, int rows, float eps,
+                                                               f16* y) {
+    typedef f16 f16x8 __attribute__((ext_vector_type(8)));
+    const int lane = threadIdx.x & 63;
+    const int w0 = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int W = gridDim.x * 4;
+    float gf[8], bf[8];
+    {
+        const f16x8 gv = *reinterpret_cast<const f16x8*>(g + lane * 8);
+        const f16x8 bv = *reinterpret_cast<const f16x8*>(bta + lane * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) gf[e] = (float)gv[e], bf[e] = (float)bv[e];
+    }
+    auto load = [&](int row) {
+        return row < rows ? *reinterpret_cast<const f16x8*>(x + (size_t)row * 512 + lane * 8) : f16x8{};
+    };
+    f16x8 buf[kLnDepth];
+#pragma unroll
+    for (int d = 0; d < kLnDepth; ++d) buf[d] = load(w0 + d * W);
+    for (int base = w0; base < rows; base += kLnDepth * W) {
+#pragma unroll
+        for (int d = 0; d < kLnDepth; ++d) {
+            const int row = base + d * W;
+            if (row >= rows) return;
+            const f16x8 xv = buf[d];
+            buf[d] = load(row + kLnDepth * W);
+            float v[8], s = 0.f, q = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                v[e] = (float)xv[e];
+                s += v[e];
+                q = fmaf(v[e], v[e], q);
+            }
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) {
+                s += __shfl_xor(s, m, 64);
+                q += __shfl_xor(q, m, 64);
+            }
+            const float mean = s * (1.f / 512);
+            const float rstd = rsqrtf(fmaxf(q * (1.f / 512) - mean * mean, 0.f) + eps);
+            const float nm = -mean * rstd;
+            f16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float t = fmaf(fmaf(v[e], rstd, nm), gf[e], bf[e]);
+                const float at = fabsf(t);
+                const float r = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, at, 1.f));
+                float p = fmaf(0.5f * 1.061405429f, r, 0.5f * -1.453152027f);
+                p = fmaf(p, r, 0.5f * 1.421413741f);
+                p = fmaf(p, r, 0.5f * -0.284496736f);
+                p = fmaf(p, r, 0.5f * 0.254829592f);
+                const float w = p * r * at;
+                const float ex = __builtin_amdgcn_exp2f(t * t * (-0.5f * 1.4426950408889634f));
+                o[e] = (f16)fmaf(-w, ex, fmaxf(t, 0.f));
+            }
+            *reinterpret_cast<f16x8*>(y + (size_t)row * 512 + lane * 8) = o;
+        }
+    }
+}
+#endif  // LG_LN_FORM == 1
+
 // ---- dual log-softmax ----
 // Pass 1 (lse_kernel): blocks [0, rb) -> row logsumexp (one wave per row); blocks [rb, ...) ->
 // column partials: a block is 64 consecutive columns x one chunk of kColChunk rows, its 256
@@ -623,8 +704,15 @@ int32_t lg_layernorm_gelu(int32_t dtype, const void* x, const void* gamma, const
     if (dtype == MHA_HD64_DT_HALF && dim == 512 &&
         ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta) |
           reinterpret_cast<uintptr_t>(y)) & 15) == 0) {
+#if LG_LN_FORM == 1
+        const int cap = 256 * kLnBlocksPerCU;
+        const int nb = (rows + 3) / 4 < cap ? (rows + 3) / 4 : cap;
+        hipLaunchKernelGGL(ln_gelu_512_rows_kernel, dim3(nb), dim3(256), 0, stream, (const f16*)x, (const f16*)gamma,
+                           (const f16*)beta, rows, eps, (f16*)y);
+#else
         hipLaunchKernelGGL(ln_gelu_512_f16_kernel, grid, dim3(256), 0, stream, (const f16*)x, (const f16*)gamma,
                            (const f16*)beta, rows, eps, (f16*)y);
+#endif
         return launched("lg_layernorm_gelu");
     }
 #define LG_LN(PER)                                                                                              \
