@@ -89,7 +89,9 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
                               float eps, void* out, hipStream_t stream);
 /* lg_linear_qkv_rotary: SelfBlock projection (lightglue.py:111-134) with W's rows and the bias in
  *                       [q|k|v][head][dim] order (row j*heads*64 + h*64 + d = Wqkv row (h*64+d)*3 + j):
- *                       rotary (cos/sin [n0+n1, 64]) on q and k, per-image head-major outputs. */
+ *                       rotary (cos/sin [n0+n1, 64]) on q and k in fp16 arithmetic, as the reference's
+ *                       fp16 model rounds t * cos + rotate_half(t) * sin (each product and the sum),
+ *                       per-image head-major outputs. */
 int32_t lg_linear_qkv_rotary(const void* x, const void* w_perm, const void* b_perm, const void* cos, const void* sin,
                              int32_t heads, int32_t n0, int32_t n1, int32_t pairs, int32_t k, void* q0, void* k0,
                              void* v0, void* q1, void* k1, void* v1, hipStream_t stream);
@@ -127,8 +129,8 @@ int32_t lg_pair_inputs(const void* desc0, const void* desc1, const void* kpts0, 
 
 /* Test and benchmark hook: the projections' tile forms for launches of many rows (several image
  * pairs per forward): 0 the 64 x 64 form only, 1 the 256 x 128 form where n allows, 2 the
- * 256 x 256 form where n allows, 3 the 256 x 256 form with a fifth ring stage (A/B only), -1 (the
- * default) chosen by size; values outside -1..3 are clamped. The environment variable
+ * 256 x 256 form where n allows (plain bias outputs; else 1), 3 the 128 x 256 form (A/B only), -1
+ * (the default) chosen by size; values outside -1..3 are clamped. The environment variable
  * LG_LINEAR_WIDE sets the initial mode the same way. Every form gives the same bits. Returns the
  * previous mode. */
 int32_t lg_linear_set_wide(int32_t mode);

@@ -100,7 +100,8 @@ __device__ __forceinline__ const f16* a_src(const LinArgs& p, int row, int gc) {
 // The projections' output arithmetic, shared by every form (so every form gives the same bits): the
 // GEMM value plus bias is rounded to fp16 once (F.linear's fp16 output, lightglue.py:97-122); the
 // residual add and the rotary (lightglue.py:124-134) then work from that value, as the reference's
-// fp16 model does (x + ffn(...), q * cos + rotate(q) * sin), in fp32 with one rounding each.
+// fp16 model does (x + ffn(...): fp32 with one rounding; q * cos + rotate(q) * sin: fp16 products
+// and sum, rot_pair).
 __device__ __forceinline__ f16 lin_val(float acc, f16 b) { return (f16)(acc + (float)b); }
 __device__ __forceinline__ f16 res_add(f16 v, f16 r) { return (f16)((float)v + (float)r); }
 // erf for the fp16 GELU: Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), as lightglue_glue.hip's
@@ -117,12 +118,19 @@ __device__ __forceinline__ float erf_as(float x) {
     return copysignf(e, x);
 }
 
-// (x0, x1) of a rotary pair (d, d + 1) -> (x0 c0 - x1 s0, x1 c1 + x0 s1), elements e, e + 1 of v
+// (x0, x1) of a rotary pair (d, d + 1) -> (x0 c0 - x1 s0, x1 c1 + x0 s1), elements e, e + 1 of v,
+// in fp16 arithmetic as the reference's fp16 model evaluates t * cos + rotate_half(t) * sin
+// (lightglue.py:124-134): each product and the sum rounded to fp16 (packed v_pk_mul_f16 /
+// v_pk_add_f16, no contraction into an fma)
+typedef f16 f16x2 __attribute__((ext_vector_type(2)));
 template <typename V>
 __device__ __forceinline__ void rot_pair(V& v, int e, f16 c0, f16 s0, f16 c1, f16 s1) {
-    const float x0 = (float)v[e], x1 = (float)v[e + 1];
-    v[e] = (f16)__builtin_fmaf(x0, (float)c0, -(x1 * (float)s0));
-    v[e + 1] = (f16)__builtin_fmaf(x1, (float)c1, x0 * (float)s1);
+#pragma clang fp contract(off)
+    const f16x2 x = f16x2{v[e], v[e + 1]};
+    const f16x2 xr = f16x2{-v[e + 1], v[e]};
+    const f16x2 o = x * f16x2{c0, c1} + xr * f16x2{s0, s1};
+    v[e] = o[0];
+    v[e + 1] = o[1];
 }
 
 template <int EPI, bool GATHER, int KC>
@@ -471,6 +479,24 @@ __global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
             if (p.m != -12345) continue;
         }
         const int hd = p.heads * kD;
+        // Head-major outputs (QKV / SPLIT2): rows rb + 32 mb + 8 i of the coalesced phase, split
+        // into (pair, row of the pair) with one division per tile and a step per row (pairs of
+        // more than 56 rows here, tile_form: one wrap at most); rows past m take row m - 1's
+        // place, as their A rows did.
+        const int ntot = p.n0 + p.n1;
+        const int rb = m0 + wm * 64 + cr;
+        const int pr0 = rb / ntot, l0 = rb - pr0 * ntot;
+        const int prl = (p.m - 1) / ntot, ll = p.m - 1 - prl * ntot;
+        auto split_row = [&](int o, int& pr, int& l) {
+            pr = pr0, l = l0 + o;
+            if (l >= ntot) l -= ntot, ++pr;
+            if (rb + o > p.m - 1) pr = prl, l = ll;
+        };
+        // (the common tile: no lane's rows rb .. rb + 56 cross an image, pair or m boundary, so row
+        // o's offset is row 0's + 64 o in the same image: wave-uniform)
+        const bool img0 = l0 < p.n0;
+        const bool span = (img0 ? l0 + 56 < p.n0 : l0 + 56 < ntot) && rb + 56 <= p.m - 1;
+        const bool easy = __builtin_amdgcn_ballot_w64(!span) == 0;
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
@@ -492,19 +518,41 @@ __global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
                     const int rl = 8 * i + cr;
                     o[i] = *(lds_f16x8*)(stg + rl * 128 + ((cc ^ (rl & 7)) << 4));
                 }
+                if constexpr (EPI == EPI_BIAS) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int row = min(m0 + wm * 64 + 32 * mb + 8 * i + cr, p.m - 1);
-                    const int n = nw0 + 64 * np + 8 * cc;  // 8 consecutive channels n..n+7
-                    f16x8 v = o[i];
-                    if constexpr (EPI == EPI_BIAS) {
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = min(m0 + wm * 64 + 32 * mb + 8 * i + cr, p.m - 1);
+                        const int n = nw0 + 64 * np + 8 * cc;  // 8 consecutive channels n..n+7
+                        f16x8 v = o[i];
                         if constexpr (RES) {
 #pragma unroll
                             for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], aux[mb][np][i][e]);
                         }
                         *reinterpret_cast<f16x8*>(p.out[0] + (size_t)row * p.n + n) = v;
+                    }
+                } else {
+                    // the wave's 64 channels lie in one head of one part (nw0 + 64 np and hd are
+                    // multiples of 64): part, head and the two images' destinations are wave-uniform
+                    const int nu = __builtin_amdgcn_readfirstlane(nw0 + 64 * np);
+                    const int part = nu / hd, h = (nu - part * hd) / kD;
+                    f16* d0;
+                    f16* d1;
+                    if constexpr (EPI == EPI_QKV_ROTARY) {
+                        d0 = part == 0 ? p.out[0] : part == 1 ? p.out[1] : p.out[2];
+                        d1 = part == 0 ? p.out[3] : part == 1 ? p.out[4] : p.out[5];
                     } else {
-                        const int part = n / hd, h = (n % hd) / kD, d = n % kD;
+                        d0 = part == 0 ? p.out[0] : p.out[2];
+                        d1 = part == 0 ? p.out[1] : p.out[3];
+                    }
+                    // element offsets in [pairs, heads, ni, 64]: pair stride, head h's first row + d
+                    const unsigned ps0 = (unsigned)(p.heads * p.n0 * kD), ps1 = (unsigned)(p.heads * p.n1 * kD);
+                    const unsigned hb0 = (unsigned)(h * p.n0 * kD + 8 * cc), hb1 = (unsigned)(h * p.n1 * kD + 8 * cc);
+                    f16* const db = img0 ? d0 : d1;
+                    const unsigned ob = img0 ? (unsigned)pr0 * ps0 + (unsigned)l0 * kD + hb0
+                                             : (unsigned)pr0 * ps1 + (unsigned)(l0 - p.n0) * kD + hb1;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        f16x8 v = o[i];
                         if constexpr (EPI == EPI_QKV_ROTARY) {
                             if (part < 2) {
 #pragma unroll
@@ -512,9 +560,16 @@ __global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
                                     rot_pair(v, e, aux[mb][0][i][e], aux2[mb][i][e], aux[mb][0][i][e + 1], aux2[mb][i][e + 1]);
                             }
                         }
-                        const LinRow lr = lin_row(p, row, h);
-                        f16* dst = p.out[(lr.first ? 0 : (EPI == EPI_QKV_ROTARY ? 3 : 1)) + (EPI == EPI_QKV_ROTARY ? part : 2 * part)];
-                        *reinterpret_cast<f16x8*>(dst + lr.off + d) = v;
+                        if (easy) {
+                            *reinterpret_cast<f16x8*>(db + ob + (unsigned)((32 * mb + 8 * i) * kD)) = v;
+                            continue;
+                        }
+                        int pr, l;
+                        split_row(32 * mb + 8 * i, pr, l);
+                        const bool first = l < p.n0;
+                        const unsigned off = first ? (unsigned)pr * ps0 + (unsigned)l * kD + hb0
+                                                   : (unsigned)pr * ps1 + (unsigned)(l - p.n0) * kD + hb1;
+                        *reinterpret_cast<f16x8*>((first ? d0 : d1) + off) = v;
                     }
                 }
             }
@@ -755,6 +810,9 @@ int tile_form(const LinArgs& p, int epi) {
     if (p.res) al = al && aligned16(p.res);
     if (epi == EPI_QKV_ROTARY) al = al && aligned16(p.cosv) && aligned16(p.sinv);
     if (!al) return 0;
+    // (the head-major epilogue's element offsets are 32-bit: every per-image output below 2^32 elements;
+    // (and it steps through the rows of a tile with one wrap at most: pairs of more than 56 rows)
+    if (epi != EPI_BIAS && ((long long)p.m * p.heads * kD >= (1LL << 32) || p.n0 + p.n1 <= 56)) return 0;
     const int w = wide_mode();
     const int f = w >= 0 ? w : ((long)((p.m + 255) / 256) * (p.n / 128) >= 128 ? 1 : 0);
     if (f == 1 && p.n % 128 == 0) return 1;
