@@ -80,10 +80,10 @@ int32_t lg_linear_cat(const void* x, const void* ctx0, const void* ctx1, int32_t
                       int32_t pairs, const void* w, const void* bias, int32_t n, void* out, hipStream_t stream);
 /* lg_linear_cat_ln_gelu: the FFN's first half (lightglue.py:101-106) after lg_linear_cat:
  *                       out [n0+n1, 512] = GELU(LayerNorm(fp16([x | merge_heads(ctx0, ctx1)] · Wᵀ + bias)))
- *                       with the LayerNorm's gamma, beta [512] and eps (exact-erf GELU). heads * 128 must
- *                       be 512 for the one-launch form (128-row tiles owning whole rows; opt-in, see
- *                       lg_linear_set_ln_fused; from 128 tiles on, 16-B aligned bias / gamma / beta / out);
- *                       otherwise (the default) lg_linear_cat then lg_layernorm_gelu in place. */
+ *                       with the LayerNorm's gamma, beta [512] and eps (exact-erf GELU). One launch
+ *                       (128-row tiles owning whole rows) from a full round of its tiles on (m >= 32,768
+ *                       rows; heads * 128 = 512, 16-B aligned bias / gamma / beta / out), else
+ *                       lg_linear_cat then lg_layernorm_gelu in place; see lg_linear_set_ln_fused. */
 int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
                               int32_t pairs, const void* w, const void* bias, const void* gamma, const void* beta,
                               float eps, void* out, hipStream_t stream);
@@ -135,9 +135,9 @@ int32_t lg_pair_inputs(const void* desc0, const void* desc1, const void* kpts0, 
  * previous mode. */
 int32_t lg_linear_set_wide(int32_t mode);
 
-/* Test and benchmark hook: 1 lets lg_linear_cat_ln_gelu take its one-launch form where it applies
- * (default 0: measured slower, csrc/lightglue_linear.hip). Same results within fp16 rounding, not the
- * same bits (its variance is two-pass). Returns the previous setting. */
+/* Test and benchmark hook for lg_linear_cat_ln_gelu's forms: 1 (the default) one launch from a full
+ * round of its tiles on, 0 always two launches, 2 always one launch (A/B). The forms agree within fp16
+ * rounding, not in every bit (the one-launch variance is two-pass). Returns the previous setting. */
 int32_t lg_linear_set_ln_fused(int32_t on);
 
 #ifdef __cplusplus

@@ -770,11 +770,14 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
 }
 
 constexpr int kTileGrid = 256;  // the 256-row forms: one workgroup per CU
-// lg_linear_cat_ln_gelu's one-launch form (linear_ln_kernel): opt-in (lg_linear_set_ln_fused). At
-// P = 16, M = 32,768 it takes 42.2 us against 25 + 17 for the two launches
-// (profiles/r05/matcher_p16_kernel_stats_ln_fused.csv): with one 128 x 512 tile per CU the ~8 k
-// cycles of GELU vector work per wave run after the GEMM, with no other wave's MFMAs beside them.
-std::atomic<int> g_ln_fused{0};
+// lg_linear_cat_ln_gelu's one-launch form (linear_ln_kernel): taken from one full round of its
+// 128-row tiles on (256: M >= 32,768 rows, P >= 16 pairs of 1024 keypoints). Measured against the two
+// launches (profiles/r05/ln_fused_by_size.jsonl): op alone 39.4 vs 42.3 us at P = 16, 72.7 vs 74.4 at
+// P = 32, but 32.2 vs 27.1 at P = 8 and 28.3 vs 9.2 at P = 1 (too few workgroups: each one's GELU vector
+// work runs after its GEMM with no other wave's MFMAs beside it); whole forwards P = 16 2.487 vs
+// 2.541 ms, P = 32 4.642 vs 4.701, P = 8 1.638 vs 1.497. lg_linear_set_ln_fused: 1 by size (default),
+// 0 always two launches, 2 always one (A/B).
+std::atomic<int> g_ln_fused{1};
 // The tile form (tile_form below): lg_linear_set_wide(0..3) or LG_LINEAR_WIDE forces one (where n
 // allows), for tests and A/B timing; -1 (the default) chooses by size.
 std::atomic<int> g_wide{-2};
@@ -907,7 +910,8 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
         !aligned8(bias) || !aligned8(out) || !(eps >= 0.f))
         return bad("lg_linear_cat_ln_gelu");
     if (m == 0) return MHA_HD64_STATUS_SUCCESS;
-    const bool fused = g_ln_fused.load() && n == kLnN && (m + 127) / 128 >= 128 && aligned16(bias) && aligned16(gamma) &&
+    const int lnf = g_ln_fused.load();  // 1: from a full round of tiles on; 2: at every size (A/B)
+    const bool fused = lnf && n == kLnN && (lnf == 2 || (m + 127) / 128 >= kTileGrid) && aligned16(bias) && aligned16(gamma) &&
                        aligned16(beta) && aligned16(out) && wide_mode() != 0;
     if (!fused) {  // the projection, then LayerNorm+GELU in place (lightglue_glue.hip)
         const int32_t st = lg_linear_cat(x, ctx0, ctx1, heads, n0, n1, pairs, w, bias, n, out, stream);
@@ -968,6 +972,6 @@ int32_t lg_linear_set_wide(int32_t mode) {
 
 int32_t lg_glue_abi_version(void) { return LG_GLUE_ABI_VERSION; }
 
-int32_t lg_linear_set_ln_fused(int32_t on) { return g_ln_fused.exchange(on ? 1 : 0); }
+int32_t lg_linear_set_ln_fused(int32_t on) { return g_ln_fused.exchange(on == 2 ? 2 : on ? 1 : 0); }
 
 }  // extern "C"

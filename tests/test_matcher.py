@@ -493,14 +493,18 @@ def test_torch_glue_runs_pairs_one_by_one():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pairs,n0,n1", [(3, 37, 70), (2, 1000, 777), (16, 1024, 1024)])
+@pytest.mark.parametrize("pairs,n0,n1", [(3, 37, 70), (2, 1000, 777), (16, 1024, 1024), (40, 20, 30), (5, 1, 63),
+                                         (4, 56, 1)])
 def test_wide_projections_equal_narrow(pairs, n0, n1):
     """The projections' 256-row tile forms (csrc/lightglue_linear.hip linear_tile_kernel: 256 x 128,
     256 x 256 and 128 x 256 tiles with the LDS-staged coalesced epilogue, taken for launches of at
     least one round of tiles: several image pairs per forward) give the bits of the 64 x 64 form on
     every fused entry point — ragged row counts (rows past m in a tile: computed on the clamped last
     row, their stores rewrite that row's bytes), both K (256 and 512), residual on and off, the
-    A-gather of lg_linear_cat, the per-image scatters."""
+    A-gather of lg_linear_cat, the per-image scatters. The head-major epilogue's row paths: the
+    per-tile row step (1024-row images), the per-row split where a lane's rows cross an image or
+    pair boundary (37 + 70, 1 + 63, 56 + 1: the shortest pair it takes), and the 64 x 64 fallback for
+    pairs of <= 56 rows (20 + 30)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from lightglue_amd import _lib
@@ -554,10 +558,11 @@ def test_wide_projections_equal_narrow(pairs, n0, n1):
 def test_linear_cat_ln_gelu_matches_torch(pairs, n0, n1):
     """lg_linear_cat_ln_gelu (the FFN's Linear -> LayerNorm -> GELU, lightglue.py:101-106) against
     the torch restatement on the same fp16 operands: F.linear rounded to fp16 (as the fp16 model
-    rounds h), then layer_norm and exact GELU in fp32; the default two-launch path and the opt-in
-    one-launch form (lg_linear_set_ln_fused(1): 128-row tiles owning whole rows, statistics in the
-    workgroup; 16 x 2048 and 9 x 2011 rows take it, 2001 rows stay on two launches). Bound: a few
-    fp16 ulps of the O(1) outputs."""
+    rounds h), then layer_norm and exact GELU in fp32; both forms, forced (lg_linear_set_ln_fused 0:
+    two launches, 2: the one-launch form, 128-row tiles owning whole rows, statistics in the
+    workgroup), and the default's choice by size (one launch from a full round of 256 tiles on:
+    16 x 2048 rows; 9 x 2011 and 2001 rows take two launches). Bound: a few fp16 ulps of the O(1)
+    outputs."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from lightglue_amd import _lib
@@ -575,9 +580,11 @@ def test_linear_cat_ln_gelu_matches_torch(pairs, n0, n1):
         ln = torch.nn.LayerNorm(512).to(dev, dt)
         ln.weight.copy_(1 + 0.1 * rnd(512))
         ln.bias.copy_(0.1 * rnd(512))
-        got = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)
-        prev = lib.lg_linear_set_ln_fused(1)
+        got = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)  # the default
+        prev = lib.lg_linear_set_ln_fused(0)
         try:
+            two = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)
+            lib.lg_linear_set_ln_fused(2)
             fused = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)
         finally:
             lib.lg_linear_set_ln_fused(prev)
@@ -585,11 +592,12 @@ def test_linear_cat_ln_gelu_matches_torch(pairs, n0, n1):
         ref = F.gelu(F.layer_norm(hh.float(), (512,), ln.weight.float(), ln.bias.float(), ln.eps))
         unf = mt._Hip.layernorm_gelu(hh, ln)  # the two-launch path
         torch.cuda.synchronize()
-    err = float((got.float() - ref).abs().max())
+    err = float((two.float() - ref).abs().max())
     err_f = float((fused.float() - ref).abs().max())
     print(f"cat+LN+GELU P={pairs}: max-abs {err:.3e} (one-launch form {err_f:.3e})")
-    assert torch.isfinite(got).all() and torch.isfinite(fused).all()
-    assert torch.equal(got, unf)  # the default path is the two launches
+    assert torch.isfinite(two).all() and torch.isfinite(fused).all()
+    assert torch.equal(two, unf)  # the two-launch form is lg_linear_cat + lg_layernorm_gelu
+    assert torch.equal(got, fused if pairs * (n0 + n1) >= 256 * 128 else two)  # the default's choice by size
     assert err <= 8e-3 and err_f <= 8e-3
 
 

@@ -1,0 +1,58 @@
+"""Timeline of the last graph-replayed forward in a rocprofv3 kernel trace of
+tools/matcher_profile.py: each kernel's duration and the idle gap before it (dispatch-to-dispatch
+seams inside the graph), summed by kernel family.
+
+    python tools/forward_timeline.py <dir>/m_kernel_trace.csv [kernels per forward]
+
+Without a count, one forward is cut at the assignment head (lse16 + combine16, once per forward)."""
+import csv
+import sys
+from collections import defaultdict
+
+
+def family(name):
+    n = name.removeprefix("void ").replace("(anonymous namespace)::", "").replace("mha_hd64::", "")
+    for k in ("mha_hd64_stream_kernel", "mha_hd64_direct16_kernel", "mha_hd64_direct_kernel", "mha_hd64_fwd_kernel",
+              "linear_tile_kernel", "linear_kernel", "ln_gelu", "lse16", "combine16", "pair_inputs", "Cijk"):
+        if k in n:
+            if k.startswith("linear"):
+                return n.split("(")[0]
+            return k
+    return "FW " + n.split("(")[0][:60]
+
+
+def main():
+    rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+    names = [r["Kernel_Name"] for r in rows]
+    per = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    if per:
+        last = rows[-per:]
+    else:  # one forward = the kernels after the second-to-last assignment head (lse16, once per forward)
+        marks = [i for i, n in enumerate(names) if "lse16" in n]
+        last = rows[marks[-2] + 1:marks[-1] + 1] if len(marks) >= 2 else rows
+        # (the last forward's head is followed by its combine pass)
+        last += [r for r in rows[marks[-1] + 1:marks[-1] + 2] if "combine16" in r["Kernel_Name"]]
+        last = last[1:] if last and "combine16" in last[0]["Kernel_Name"] else last
+        per = len(last)
+    t0 = int(last[0]["Start_Timestamp"])
+    t1 = int(last[-1]["End_Timestamp"])
+    busy = defaultdict(float)
+    gaps = defaultdict(float)
+    count = defaultdict(int)
+    prev_end = None
+    for r in last:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        f = family(r["Kernel_Name"])
+        busy[f] += (e - s) / 1e3
+        count[f] += 1
+        if prev_end is not None:
+            gaps[f] += max(0, s - prev_end) / 1e3
+        prev_end = e
+    print(f"kernels per forward {per}; forward {(t1 - t0) / 1e3:.1f} us; kernel time {sum(busy.values()):.1f} us; "
+          f"gaps {sum(gaps.values()):.1f} us")
+    for f in sorted(busy, key=lambda k: -busy[k]):
+        print(f"{busy[f]:8.1f} us busy {gaps[f]:7.1f} us gap before  {count[f]:3d} x  {f}")
+
+
+if __name__ == "__main__":
+    main()
