@@ -6,7 +6,8 @@ replay of back-to-back launches, interleaved; TFLOP/s of each.
 
 With a fifth argument "b": yardsticks in the same run -- torch.nn.functional.linear (hipBLASLt,
 fp16, plain [M, N] output + bias) on the op's M / K / N, and a device copy of the op's algorithmic
-bytes (its HBM roofline at the copy rate); yardsticks only, never a product path."""
+bytes (its HBM roofline at the copy rate); yardsticks only, never a product path. "cat_ln_gelu" is
+lg_linear_cat_ln_gelu (its form by size; the mode list only switches the projection forms)."""
 import json
 import os
 import statistics
@@ -39,11 +40,13 @@ def main():
     w2, b2 = torch.randn(512, 256, device=dev, dtype=dt) * 0.05, torch.randn(512, device=dev, dtype=dt)
     w3, b3 = torch.randn(512, 512, device=dev, dtype=dt) * 0.05, torch.randn(512, device=dev, dtype=dt)
     w4, b4 = torch.randn(256, 512, device=dev, dtype=dt) * 0.05, torch.randn(256, device=dev, dtype=dt)
+    ln = torch.nn.LayerNorm(512).to(dev, dt)
     ops = {
         "qkv_rotary k256 n768": (lambda: mt._Hip.linear_qkv_rotary(x, w768, b768, cos, sin, h, sp), 256 * 768),
         "split2 k256 n512": (lambda: mt._Hip.linear_split2(x, w2, b2, h, sp), 256 * 512),
         "cat k512 n512": (lambda: mt._Hip.linear_cat(x, c0, c1, w3, b3), 512 * 512),
         "linear+res k512 n256": (lambda: mt._Hip.linear(hx, w4, b4, x), 512 * 256),
+        "cat_ln_gelu k512 n512": (lambda: mt._Hip.linear_cat_ln_gelu(x, c0, c1, w3, b3, ln), 512 * 512),
     }
     # algorithmic bytes per op: A + W + bias + outputs (+ cos/sin, + residual)
     nbytes = {
@@ -51,6 +54,7 @@ def main():
         "split2 k256 n512": 2 * (M * 256 + 512 * 256 + 512 + M * 512),
         "cat k512 n512": 2 * (M * 512 + 512 * 512 + 512 + M * 512),
         "linear+res k512 n256": 2 * (M * 512 + 256 * 512 + 256 + 2 * M * 256),
+        "cat_ln_gelu k512 n512": 2 * (M * 512 + 512 * 512 + 3 * 512 + M * 512),
     }
     blas = {}
     if yard:
@@ -60,6 +64,7 @@ def main():
             "split2 k256 n512": lambda: torch.nn.functional.linear(xa, w2, b2),
             "cat k512 n512": lambda: torch.nn.functional.linear(xb, w3, b3),
             "linear+res k512 n256": lambda: torch.nn.functional.linear(xb, w4, b4),
+            "cat_ln_gelu k512 n512": lambda: torch.nn.functional.linear(xb, w3, b3),
         }
         pool = torch.empty(2 * max(nbytes.values()) // 2 + 16, dtype=torch.uint8, device=dev)
     st = torch.cuda.Stream(dev)
