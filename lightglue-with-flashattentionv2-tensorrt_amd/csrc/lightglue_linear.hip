@@ -47,6 +47,14 @@ typedef __attribute__((address_space(3))) f16x8 lds_f16x8;
 #ifndef LG_ABL
 #define LG_ABL 0
 #endif
+// (A/B build: -DLG_ST_NT=1 makes the 256-row forms' output stores non-temporal)
+#ifndef LG_ST_NT
+#define LG_ST_NT 0
+#endif
+__device__ __forceinline__ void st_out(f16* dst, f16x8 v) {
+    if constexpr (LG_ST_NT) __builtin_nontemporal_store(v, reinterpret_cast<f16x8*>(dst));
+    else *reinterpret_cast<f16x8*>(dst) = v;
+}
 constexpr int kBM = 64, kBN = 64, kKC = 128;
 // tile rows, tile channels, K columns per LDS chunk
 constexpr int kChunkBytes = 64 * kKC * 2;     // one [64 rows][128 k] fp16 chunk = 16 KiB
@@ -528,7 +536,7 @@ __global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
 #pragma unroll
                             for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], aux[mb][np][i][e]);
                         }
-                        *reinterpret_cast<f16x8*>(p.out[0] + (size_t)row * p.n + n) = v;
+                        st_out(p.out[0] + (size_t)row * p.n + n, v);
                     }
                 } else {
                     // the wave's 64 channels lie in one head of one part (nw0 + 64 np and hd are
@@ -561,7 +569,7 @@ __global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
                             }
                         }
                         if (easy) {
-                            *reinterpret_cast<f16x8*>(db + ob + (unsigned)((32 * mb + 8 * i) * kD)) = v;
+                            st_out(db + ob + (unsigned)((32 * mb + 8 * i) * kD), v);
                             continue;
                         }
                         int pr, l;
@@ -569,7 +577,7 @@ __global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
                         const bool first = l < p.n0;
                         const unsigned off = first ? (unsigned)pr * ps0 + (unsigned)l * kD + hb0
                                                    : (unsigned)pr * ps1 + (unsigned)(l - p.n0) * kD + hb1;
-                        *reinterpret_cast<f16x8*>((first ? d0 : d1) + off) = v;
+                        st_out((first ? d0 : d1) + off, v);
                     }
                 }
             }
@@ -760,7 +768,7 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int row = min(m0 + wm * 64 + 32 * mb + 8 * i + cr, p.m - 1);
-                    *reinterpret_cast<f16x8*>(p.out[0] + (size_t)row * NT + nw0 + 64 * np + 8 * cc) = o8[i];
+                    st_out(p.out[0] + (size_t)row * NT + nw0 + 64 * np + 8 * cc, o8[i]);
                 }
             }
         }
