@@ -167,18 +167,38 @@ __global__ __launch_bounds__(256) void ln_gelu_kernel(const T* __restrict__ x, c
     }
 }
 
-// erf for the fp16 GELU: Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below the fp16
-// rounding of the output), one v_rcp_f32 and one v_exp_f32 instead of the library erff's branches
-__device__ __forceinline__ float erf_as(float x) {
-    const float a = fabsf(x);
-    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
-    float y = fmaf(1.061405429f, t, -1.453152027f);
-    y = fmaf(y, t, 1.421413741f);
-    y = fmaf(y, t, -0.284496736f);
-    y = fmaf(y, t, 0.254829592f);
-    y *= t;
-    const float e = 1.f - y * __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);
-    return copysignf(e, x);
+// Exact (erf) GELU for the fp16 FFN with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far
+// below the fp16 rounding of the output), folded: with z = |x| / sqrt(2), r = 1 / (1 + p z) and
+// erf(z) = 1 - y(r) e^{-z^2}, x Phi(x) = max(x, 0) - |x| (y / 2) e^{-x^2 / 2} for either sign of x (no
+// 1 + erf cancellation for negative x); one v_rcp_f32 and one v_exp_f32, the 1/2 and 1/sqrt(2) in
+// the constants. (lightglue_glue.hip and lightglue_linear.hip compute it alike.)
+__device__ __forceinline__ float gelu_as(float x) {
+    const float ax = fabsf(x);
+    const float r = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, ax, 1.f));
+    float p = fmaf(0.5f * 1.061405429f, r, 0.5f * -1.453152027f);
+    p = fmaf(p, r, 0.5f * 1.421413741f);
+    p = fmaf(p, r, 0.5f * -0.284496736f);
+    p = fmaf(p, r, 0.5f * 0.254829592f);
+    const float w = p * r * ax;
+    const float e = __builtin_amdgcn_exp2f(x * x * (-0.5f * 1.4426950408889634f));
+    return fmaf(-w, e, fmaxf(x, 0.f));
+}
+// The same on a pair of values, written on float2 so that the FMAs and products issue as packed
+// v_pk_fma_f32 / v_pk_mul_f32 (two values per instruction: the vector pipe's full fp32 rate; the
+// rcp, exp, abs and max stay per value)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_as2(f32x2 x) {
+    const f32x2 ax = f32x2{fabsf(x[0]), fabsf(x[1])};
+    const f32x2 den = ax * (0.3275911f * 0.70710678118654752f) + 1.f;
+    const f32x2 r = f32x2{__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+    f32x2 p = r * (0.5f * 1.061405429f) + (0.5f * -1.453152027f);
+    p = p * r + (0.5f * 1.421413741f);
+    p = p * r + (0.5f * -0.284496736f);
+    p = p * r + (0.5f * 0.254829592f);
+    const f32x2 w = p * r * ax;
+    const f32x2 a = x * x * (-0.5f * 1.4426950408889634f);
+    const f32x2 e = f32x2{__builtin_amdgcn_exp2f(a[0]), __builtin_amdgcn_exp2f(a[1])};
+    return f32x2{fmaxf(x[0], 0.f), fmaxf(x[1], 0.f)} - w * e;
 }
 
 // fp16, dim 512 (the matcher's FFN width): a lane owns 8 contiguous columns (one 16-B load of x,
@@ -209,9 +229,12 @@ __global__ __launch_bounds__(256) void ln_gelu_512_f16_kernel(const f16* __restr
     const float rstd = rsqrtf(fmaxf(q * (1.f / 512) - mean * mean, 0.f) + eps);
     f16x8 o;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const float t = (v[e] - mean) * rstd * (float)gv[e] + (float)bv[e];
-        o[e] = (f16)(0.5f * t * (1.f + erf_as(t * 0.70710678118654752f)));
+    for (int e = 0; e < 8; e += 2) {
+        const f32x2 t = (f32x2{v[e], v[e + 1]} - mean) * rstd * f32x2{(float)gv[e], (float)gv[e + 1]} +
+                        f32x2{(float)bv[e], (float)bv[e + 1]};
+        const f32x2 gl = gelu_as2(t);
+        o[e] = (f16)gl[0];
+        o[e + 1] = (f16)gl[1];
     }
     *reinterpret_cast<f16x8*>(y + (size_t)row * 512 + lane * 8) = o;
 }
@@ -219,7 +242,7 @@ __global__ __launch_bounds__(256) void ln_gelu_512_f16_kernel(const f16* __restr
 // A/B build only (SRC=glue tools/build_linear_variant.sh <name> -DLG_LN_FORM=1, tools/ln_ab.py): the
 // same operator, persistent: wave w of W walks rows w, w + W, ... with the loads of its next DEPTH
 // rows in flight while it computes one, gamma / beta converted once per wave, and GELU as
-// max(t, 0) - |t| * (y / 2) * exp(-t^2 / 2) (the same A&S 7.1.26 terms as erf_as, folded: for t >= 0
+// max(t, 0) - |t| * (y / 2) * exp(-t^2 / 2) (gelu_as, written out: for t >= 0
 // t * Phi(t) = t - t * (y e / 2), for t < 0 it is -|t| * (y e / 2); no 1 + erf cancellation).
 // Measured no faster (16.9-19.2 vs 17.0 us at 32,768 rows, profiles/r05/ln_gelu_persistent_ab.jsonl):
 // the per-row kernel is vector-issue bound, not latency bound.

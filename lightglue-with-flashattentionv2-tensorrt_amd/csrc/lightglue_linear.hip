@@ -38,6 +38,7 @@ typedef f16 f16x8 __attribute__((ext_vector_type(8)));
 typedef f16 f16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) char lds_char;
 typedef __attribute__((address_space(3))) f16x8 lds_f16x8;
 
@@ -112,18 +113,38 @@ __device__ __forceinline__ const f16* a_src(const LinArgs& p, int row, int gc) {
 // and sum, rot_pair).
 __device__ __forceinline__ f16 lin_val(float acc, f16 b) { return (f16)(acc + (float)b); }
 __device__ __forceinline__ f16 res_add(f16 v, f16 r) { return (f16)((float)v + (float)r); }
-// erf for the fp16 GELU: Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), as lightglue_glue.hip's
-// LayerNorm+GELU kernel computes it
-__device__ __forceinline__ float erf_as(float x) {
-    const float a = fabsf(x);
-    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
-    float y = fmaf(1.061405429f, t, -1.453152027f);
-    y = fmaf(y, t, 1.421413741f);
-    y = fmaf(y, t, -0.284496736f);
-    y = fmaf(y, t, 0.254829592f);
-    y *= t;
-    const float e = 1.f - y * __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);
-    return copysignf(e, x);
+// Exact (erf) GELU for the fp16 FFN with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far
+// below the fp16 rounding of the output), folded: with z = |x| / sqrt(2), r = 1 / (1 + p z) and
+// erf(z) = 1 - y(r) e^{-z^2}, x Phi(x) = max(x, 0) - |x| (y / 2) e^{-x^2 / 2} for either sign of x (no
+// 1 + erf cancellation for negative x); one v_rcp_f32 and one v_exp_f32, the 1/2 and 1/sqrt(2) in
+// the constants. (lightglue_glue.hip and lightglue_linear.hip compute it alike.)
+__device__ __forceinline__ float gelu_as(float x) {
+    const float ax = fabsf(x);
+    const float r = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, ax, 1.f));
+    float p = fmaf(0.5f * 1.061405429f, r, 0.5f * -1.453152027f);
+    p = fmaf(p, r, 0.5f * 1.421413741f);
+    p = fmaf(p, r, 0.5f * -0.284496736f);
+    p = fmaf(p, r, 0.5f * 0.254829592f);
+    const float w = p * r * ax;
+    const float e = __builtin_amdgcn_exp2f(x * x * (-0.5f * 1.4426950408889634f));
+    return fmaf(-w, e, fmaxf(x, 0.f));
+}
+// The same on a pair of values, written on float2 so that the FMAs and products issue as packed
+// v_pk_fma_f32 / v_pk_mul_f32 (two values per instruction: the vector pipe's full fp32 rate; the
+// rcp, exp, abs and max stay per value)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_as2(f32x2 x) {
+    const f32x2 ax = f32x2{fabsf(x[0]), fabsf(x[1])};
+    const f32x2 den = ax * (0.3275911f * 0.70710678118654752f) + 1.f;
+    const f32x2 r = f32x2{__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+    f32x2 p = r * (0.5f * 1.061405429f) + (0.5f * -1.453152027f);
+    p = p * r + (0.5f * 1.421413741f);
+    p = p * r + (0.5f * -0.284496736f);
+    p = p * r + (0.5f * 0.254829592f);
+    const f32x2 w = p * r * ax;
+    const f32x2 a = x * x * (-0.5f * 1.4426950408889634f);
+    const f32x2 e = f32x2{__builtin_amdgcn_exp2f(a[0]), __builtin_amdgcn_exp2f(a[1])};
+    return f32x2{fmaxf(x[0], 0.f), fmaxf(x[1], 0.f)} - w * e;
 }
 
 // (x0, x1) of a rotary pair (d, d + 1) -> (x0 c0 - x1 s0, x1 c1 + x0 s1), elements e, e + 1 of v,
@@ -139,6 +160,25 @@ __device__ __forceinline__ void rot_pair(V& v, int e, f16 c0, f16 s0, f16 c1, f1
     const f16x2 o = x * f16x2{c0, c1} + xr * f16x2{s0, s1};
     v[e] = o[0];
     v[e + 1] = o[1];
+}
+
+// Mixed-precision FMAs for the one-launch LayerNorm epilogue (fp16 operands read in place, halves
+// chosen by op_sel): mixf(x, g, b) = x * g + b in fp32 with g, b the HI-th halves of packed fp16
+// words; mixh(acc, b) = fp16(acc + b), rounded once (the two-launch path's lin_val rounds to fp32
+// first: the forms agree within the rare double-rounding ulp, not in every bit).
+template <int HI>
+__device__ __forceinline__ float mixf(float x, unsigned g2, unsigned b2) {
+    float r;
+    if constexpr (HI) asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[0,1,1]" : "=v"(r) : "v"(x), "v"(g2), "v"(b2));
+    else asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(x), "v"(g2), "v"(b2));
+    return r;
+}
+template <int HI>
+__device__ __forceinline__ float mixh(float acc, unsigned b2) {
+    unsigned h;
+    if constexpr (HI) asm("v_fma_mixlo_f16 %0, %1, 1.0, %2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(h) : "v"(acc), "v"(b2));
+    else asm("v_fma_mixlo_f16 %0, %1, 1.0, %2 op_sel_hi:[0,0,1]" : "=v"(h) : "v"(acc), "v"(b2));
+    return (float)__builtin_bit_cast(f16x2, h)[0];
 }
 
 template <int EPI, bool GATHER, int KC>
@@ -698,10 +738,11 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
             for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + (nw0 + 32 * nb + 8 * g + 4 * hh) * 2);
+                    const u32x2 b4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + (nw0 + 32 * nb + 8 * g + 4 * hh) * 2);
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        const float h = (float)lin_val(acc[nb][mb][4 * g + u], b4[u]);
+                        const float a = acc[nb][mb][4 * g + u];
+                        const float h = (u & 1) ? mixh<1>(a, b4[u >> 1]) : mixh<0>(a, b4[u >> 1]);
                         acc[nb][mb][4 * g + u] = h;
                         s += h;
                     }
@@ -727,6 +768,7 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
                     const float d = acc[nb][mb][e] - mean[mb];
+                    acc[nb][mb][e] = d;  // (h - mean, reused by the normalisation)
                     q = __builtin_fmaf(d, d, q);
                 }
             rs[mb] = q + __shfl_xor(q, 32, 64);
@@ -749,13 +791,16 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
 #pragma unroll
                     for (int g = 0; g < 4; ++g) {
                         const int n = nw0 + 64 * np + 32 * nbl + 8 * g + 4 * hh;
-                        const f16x4 g4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + NT * 2 + n * 2);
-                        const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + 2 * NT * 2 + n * 2);
+                        const u32x2 g4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + NT * 2 + n * 2);
+                        const u32x2 b4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + 2 * NT * 2 + n * 2);
                         f16x4 o;
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const float x = (acc[2 * np + nbl][mb][4 * g + u] - mean[mb]) * rstd * (float)g4[u] + (float)b4[u];
-                            o[u] = (f16)(0.5f * x * (1.f + erf_as(x * 0.70710678118654752f)));
+                        for (int u = 0; u < 4; u += 2) {
+                            const f32x16& av = acc[2 * np + nbl][mb];
+                            const f32x2 xr = f32x2{av[4 * g + u], av[4 * g + u + 1]} * rstd;
+                            const f32x2 gl = gelu_as2(f32x2{mixf<0>(xr[0], g4[u >> 1], b4[u >> 1]), mixf<1>(xr[1], g4[u >> 1], b4[u >> 1])});
+                            o[u] = (f16)gl[0];
+                            o[u + 1] = (f16)gl[1];
                         }
                         *(__attribute__((address_space(3))) f16x4*)(stg + r * 128 + (((4 * nbl + g) ^ (r & 7)) << 4) + 8 * hh) = o;
                     }
