@@ -48,6 +48,10 @@ typedef __attribute__((address_space(3))) f16x8 lds_f16x8;
 #ifndef LG_ABL
 #define LG_ABL 0
 #endif
+// (ablation build: -DLG_LN_ABL=1 drops the one-launch FFN kernel's normalisation and GELU)
+#ifndef LG_LN_ABL
+#define LG_LN_ABL 0
+#endif
 // (A/B build: -DLG_ST_NT=1 makes the 256-row forms' output stores non-temporal)
 #ifndef LG_ST_NT
 #define LG_ST_NT 0
@@ -797,6 +801,11 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
 #pragma unroll
                         for (int u = 0; u < 4; u += 2) {
                             const f32x16& av = acc[2 * np + nbl][mb];
+                            if constexpr (LG_LN_ABL & 1) {  // (ablation: no normalisation / GELU)
+                                o[u] = (f16)av[4 * g + u];
+                                o[u + 1] = (f16)av[4 * g + u + 1];
+                                continue;
+                            }
                             const f32x2 xr = f32x2{av[4 * g + u], av[4 * g + u + 1]} * rstd;
                             const f32x2 gl = gelu_as2(f32x2{mixf<0>(xr[0], g4[u >> 1], b4[u >> 1]), mixf<1>(xr[1], g4[u >> 1], b4[u >> 1])});
                             o[u] = (f16)gl[0];
