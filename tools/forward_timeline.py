@@ -13,9 +13,9 @@ from collections import defaultdict
 def family(name):
     n = name.removeprefix("void ").replace("(anonymous namespace)::", "").replace("mha_hd64::", "")
     for k in ("mha_hd64_stream_kernel", "mha_hd64_direct16_kernel", "mha_hd64_direct_kernel", "mha_hd64_fwd_kernel",
-              "linear_tile_kernel", "linear_kernel", "ln_gelu", "lse16", "combine16", "pair_inputs", "Cijk"):
+              "linear_tile_kernel", "linear_kernel", "linear_ln_kernel", "ln_gelu", "lse16", "combine16", "pair_inputs", "Cijk"):
         if k in n:
-            if k.startswith("linear"):
+            if k.startswith("linear") and k != "linear_ln_kernel":
                 return n.split("(")[0]
             return k
     return "FW " + n.split("(")[0][:60]
