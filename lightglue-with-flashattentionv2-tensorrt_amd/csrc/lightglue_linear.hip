@@ -641,12 +641,36 @@ __global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
 // (two passes over registers: the unfused kernel's E[h^2] - mean^2 cancels less well), then
 // GELU(LN(h)) (the erf of A&S 7.1.26, as the unfused fp16 kernel) rounded to fp16, staged and
 // stored as in linear_tile_kernel. bias, gamma and beta sit in LDS for the whole launch.
+// Diagnostic build (-DLG_LN_STAMPS, tools/ln_stamps.py; never shipped): per wave, s_memtime cycles
+// of linear_ln_kernel by chained segment (0 prologue, 1 K-step waits + barriers, 2 K-step DMA issue +
+// fragment reads + MFMAs, 3 epilogue: h and row statistics, 4 epilogue: normalise, GELU, staging,
+// stores), read back by lg_diag_ln_stamps.
+#ifdef LG_LN_STAMPS
+__device__ unsigned long long g_ln_stamps[256 * 8 * 8];
+#define LN_SEG(k)                                                                                    \
+    do {                                                                                             \
+        unsigned long long t_;                                                                       \
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        sg_[k] += t_ - last_;                                                                        \
+        last_ = t_;                                                                                  \
+    } while (0)
+#else
+#define LN_SEG(k) \
+    do {          \
+    } while (0)
+#endif
 constexpr int kLnN = 512;
-template <int KS>
+// the one-launch form's tile: 128 rows, 32-deep K steps, 3 stages (A/B build -DLG_LN_MT=64: 64 rows,
+// 64-deep steps, 2 stages of 72 KiB, twice the tiles per workgroup)
+#ifndef LG_LN_MT
+#define LG_LN_MT 128
+#endif
+constexpr int kLnMT = LG_LN_MT, kLnBK = LG_LN_MT == 64 ? 64 : 32, kLnNST = LG_LN_MT == 64 ? 2 : 3;
+template <int KS, int MT, int BK, int NST>
 __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16* __restrict__ gamma,
                                                            const f16* __restrict__ beta, float eps) {
-    constexpr int MT = 128, NT = kLnN, BK = 32, NST = 3;
-    constexpr int WM = 2, WN = 4, WTN = NT / WN, NB = WTN / 32, NP = WTN / 64;
+    constexpr int NT = kLnN;
+    constexpr int WM = MT / 64, WN = 8 / WM, WTN = NT / WN, NB = WTN / 32, NP = WTN / 64;
     constexpr int SB = (MT + NT) * BK * 2;                             // 40 KiB
     constexpr int NWP = NT * BK * 2 / 8192, NAP = MT * BK * 2 / 8192;  // 4 + 1 pieces per wave and step
     constexpr int D = NWP + NAP;
@@ -668,6 +692,11 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
     if (j0 >= je) return;
     const int ntile_w = (je - j0 + G - 1) / G;
     const int nsteps = ntile_w * KS;
+#ifdef LG_LN_STAMPS
+    unsigned long long sg_[5] = {0, 0, 0, 0, 0}, last_, t_entry_;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_entry_)::"memory");
+    last_ = t_entry_;
+#endif
 
     auto src_of = [&](int t) { return tile_src<true, BK, NWP, NAP, 8>(p, (j0 + G * t) * MT, 0, wave, lane); };
     // the vectors into LDS (loaded ahead of the first stages, written after them: the compiler's wait
@@ -680,7 +709,7 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
     for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, 8>(cur, i, smem + i * SB, wave);
     if (tid < 192) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
 
-    auto swz = [](int row) { return (row >> 2) & 3; };
+    auto swz = [](int row) { return BK == 64 ? (row >> 1) & 7 : (row >> 2) & 3; };
     unsigned wro[NB], aro[2];
     int wsw[NB], asw[2];
 #pragma unroll
@@ -695,6 +724,15 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
     }
     const int cr = lane >> 3, cc = lane & 7;
     float* const red = (float*)(void*)(smem + kRed);  // [pass][row][wn]
+    auto red_sum = [&](int off) {  // the WN partials of a row, in a fixed order
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < WN; q += 4) {
+            const f32x4 w4 = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (off + q) * 4);
+            v += (w4[0] + w4[1]) + (w4[2] + w4[3]);
+        }
+        return v;
+    };
     int st = 0;
     for (int t = 0; t < ntile_w; ++t) {
         const int m0 = (j0 + G * t) * MT;
@@ -704,10 +742,13 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
 #pragma unroll 2
         for (int ks = 0; ks < KS; ++ks) {
             const int gs = t * KS + ks;
+            if (ks == 0 && t == 0) LN_SEG(0);
+            else LN_SEG(2);
             if (gs + NST - 2 > nsteps - 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             else if (ks < NST - 1 && t > 0) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * D + SPW) : "memory");
             else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * D) : "memory");
             __builtin_amdgcn_s_barrier();
+            LN_SEG(1);
             {
                 char* const fb = smem + (st == 0 ? NST - 1 : st - 1) * SB;
                 if (ks + NST - 1 < KS) tile_issue<true, BK, KS, NT, 8>(cur, ks + NST - 1, fb, wave);
@@ -732,6 +773,7 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
             }
         }
 
+        LN_SEG(2);
         // ---- epilogue: h = fp16(acc + bias) (lane: row wm*64 + 32 mb + r, 64 of the wave's channels) ----
         const int nw0 = wn * WTN;
         float rs[2];
@@ -764,8 +806,7 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
         float mean[2];
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb) {
-            const f32x4 v = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (wm * 64 + 32 * mb + r) * WN * 4);
-            mean[mb] = ((v[0] + v[1]) + (v[2] + v[3])) * (1.f / kLnN);
+            mean[mb] = red_sum((wm * 64 + 32 * mb + r) * WN) * (1.f / kLnN);
             float q = 0.f;
 #pragma unroll
             for (int nb = 0; nb < NB; ++nb)
@@ -783,11 +824,11 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // (also: every wave is done reading the last stage)
+        LN_SEG(3);
         lds_char* const stg = lds + st_last * SB + wave * 4096;
 #pragma unroll
         for (int mb = 0; mb < 2; ++mb) {
-            const f32x4 v = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (MT * WN + (wm * 64 + 32 * mb + r) * WN) * 4);
-            const float rstd = __builtin_amdgcn_rsqf(((v[0] + v[1]) + (v[2] + v[3])) * (1.f / kLnN) + eps);
+            const float rstd = __builtin_amdgcn_rsqf(red_sum(MT * WN + (wm * 64 + 32 * mb + r) * WN) * (1.f / kLnN) + eps);
 #pragma unroll
             for (int np = 0; np < NP; ++np) {
 #pragma unroll
@@ -829,6 +870,15 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
         if (more) cur = src_of(t + 1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    LN_SEG(4);
+#ifdef LG_LN_STAMPS
+    if (lane == 0) {
+        unsigned long long* d = g_ln_stamps + ((size_t)blockIdx.x * 8 + wave) * 8;
+        for (int k = 0; k < 5; ++k) d[k] = sg_[k];
+        d[5] = last_ - t_entry_;
+        d[6] = (unsigned long long)ntile_w;
+    }
+#endif
 }
 
 constexpr int kTileGrid = 256;  // the 256-row forms: one workgroup per CU
@@ -984,11 +1034,11 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
     p.a = (const f16*)x, p.ctx0 = (const f16*)ctx0, p.ctx1 = (const f16*)ctx1, p.w = (const f16*)w;
     p.bias = (const f16*)bias, p.out[0] = (f16*)out;
     p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
-    p.mtiles = (m + 127) / 128;
+    p.mtiles = (m + kLnMT - 1) / kLnMT;
     p.total = p.mtiles;
     const int grid = p.total < kTileGrid ? p.total : kTileGrid;
-    hipLaunchKernelGGL((linear_ln_kernel<512 / 32>), dim3(grid), dim3(512), 0, stream, p, (const f16*)gamma,
-                       (const f16*)beta, eps);
+    hipLaunchKernelGGL((linear_ln_kernel<512 / kLnBK, kLnMT, kLnBK, kLnNST>), dim3(grid), dim3(512), 0, stream, p,
+                       (const f16*)gamma, (const f16*)beta, eps);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_linear_cat_ln_gelu",
@@ -1034,6 +1084,11 @@ int32_t lg_linear_set_wide(int32_t mode) {
 
 int32_t lg_glue_abi_version(void) { return LG_GLUE_ABI_VERSION; }
 
+#ifdef LG_LN_STAMPS
+int32_t lg_diag_ln_stamps(void* host_dst) {  // (diagnostic build only: not in the header)
+    return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(g_ln_stamps), sizeof(g_ln_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
 int32_t lg_linear_set_ln_fused(int32_t on) { return g_ln_fused.exchange(on == 2 ? 2 : on ? 1 : 0); }
 
 }  // extern "C"
