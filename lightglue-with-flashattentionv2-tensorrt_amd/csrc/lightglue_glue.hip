@@ -436,7 +436,8 @@ struct DsArgs {
     long zps, zrs;
     float* scores;             // [batch, m, n]
     float* lse_row;            // workspace: [batch][m]
-    float2* col_part;          // workspace: [batch][m / 64][n]
+    float2* col_part;          // workspace: [batch][rblocks][n]
+    float* cterm;              // workspace (small launches): [batch][n] logsig(z1) - column logsumexp
     int m, n, rblocks;
 };
 
@@ -452,8 +453,10 @@ __device__ __forceinline__ void lse_step(float& mx, float& s, float v) {  // onl
 constexpr int kDsBatch = 8;  // rows a wave loads at once (16 KiB in flight per wave at n = 1024)
 constexpr int kDsWaves = 8;  // waves per block: kDsRows / kDsWaves = one batch of rows each
 
-template <int CPL>  // columns per lane in units of 8 (n <= 512 CPL)
-__global__ __launch_bounds__(64 * kDsWaves) void lse16_kernel(DsArgs a) {
+// W waves per block, kDsBatch rows each (W = kDsWaves: 64-row blocks; W = 1: 8-row blocks, the small
+// launches' form: a single pair's 1024 rows as 128 blocks instead of 16)
+template <int CPL, int W>  // columns per lane in units of 8 (n <= 512 CPL)
+__global__ __launch_bounds__(64 * W) void lse16_kernel(DsArgs a) {
     typedef f16 f16x8 __attribute__((ext_vector_type(8)));
     const int p = blockIdx.y, rb = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -463,8 +466,8 @@ __global__ __launch_bounds__(64 * kDsWaves) void lse16_kernel(DsArgs a) {
     for (int c = 0; c < CPL; ++c)
 #pragma unroll
         for (int e = 0; e < 8; ++e) cm[c][e] = -INFINITY, cs[c][e] = 0.f;
-    const int r0 = rb * kDsRows + wave * (kDsRows / kDsWaves);
-    const int r1 = min(r0 + kDsRows / kDsWaves, a.m);
+    const int r0 = (rb * W + wave) * kDsBatch;
+    const int r1 = min(r0 + kDsBatch, a.m);
     for (int i0 = r0; i0 < r1; i0 += kDsBatch) {
         // a batch of rows, every load issued first (rows past the block's end: -inf)
         f16x8 x[kDsBatch][CPL];
@@ -524,31 +527,65 @@ __global__ __launch_bounds__(64 * kDsWaves) void lse16_kernel(DsArgs a) {
             }
     }
     // the waves' column partials -> one per (block, column)
-    __shared__ float2 part[kDsWaves][64 * 8];
+    __shared__ float2 part[W][64 * 8];
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) part[wave][lane * 8 + e] = make_float2(cm[c][e], cs[c][e]);
         __syncthreads();
-        for (int t = threadIdx.x; t < 512; t += 64 * kDsWaves) {
+        for (int t = threadIdx.x; t < 512; t += 64 * W) {
             const int j = c * 512 + t;
             float mx = part[0][t].x, s = part[0][t].y;
 #pragma unroll
-            for (int w = 1; w < kDsWaves; ++w) lse_merge(mx, s, part[w][t].x, part[w][t].y);
+            for (int w = 1; w < W; ++w) lse_merge(mx, s, part[w][t].x, part[w][t].y);
             if (j < a.n) a.col_part[((size_t)p * a.rblocks + rb) * a.n + j] = make_float2(mx, s);
         }
         __syncthreads();
     }
 }
 
-template <int CPL>
-__global__ __launch_bounds__(64 * kDsWaves) void combine16_kernel(DsArgs a) {
+// The small launches' column pass: a block is 64 columns of one pair x 16 groups of row-block
+// partials (merged in a fixed order: group g takes partials g, g + 16, ...; then groups 0..15), written
+// once as logsig(z1[j]) - lse_col[j] for combine16_kernel<PRE>.
+constexpr int kColGroups = 16;
+__global__ __launch_bounds__(64 * kColGroups) void col_lse_kernel(DsArgs a) {
+    const int p = blockIdx.y, j = blockIdx.x * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+    float mx = -INFINITY, s = 0.f;
+    if (j < a.n) {
+        for (int b0 = g; b0 < a.rblocks; b0 += kColGroups * 8) {
+            float2 q[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int b = b0 + kColGroups * u;
+                q[u] = b < a.rblocks ? a.col_part[((size_t)p * a.rblocks + b) * a.n + j] : make_float2(-INFINITY, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) lse_merge(mx, s, q[u].x, q[u].y);
+        }
+    }
+    __shared__ float2 part[kColGroups][64];
+    part[g][threadIdx.x & 63] = make_float2(mx, s);
+    __syncthreads();
+    if (g == 0 && j < a.n) {
+#pragma unroll
+        for (int w = 1; w < kColGroups; ++w) lse_merge(mx, s, part[w][threadIdx.x].x, part[w][threadIdx.x].y);
+        a.cterm[(size_t)p * a.n + j] = log_sigmoid((float)a.z1[p * a.zps + j * a.zrs]) - (logf(s) + mx);
+    }
+}
+
+// PRE: the column terms come from col_lse_kernel (a.cterm), else every block merges the partials
+template <int CPL, int W, bool PRE>
+__global__ __launch_bounds__(64 * W) void combine16_kernel(DsArgs a) {
     typedef f16 f16x8 __attribute__((ext_vector_type(8)));
     typedef float f32x4 __attribute__((ext_vector_type(4)));
     const int p = blockIdx.y, rb = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     __shared__ float cterm[512 * CPL];  // logsig(z1[j]) - lse_col[j]
-    for (int j = threadIdx.x; j < a.n; j += 64 * kDsWaves) {
+    if constexpr (PRE) {
+        for (int j = threadIdx.x * 4; j < a.n; j += 64 * W * 4)
+            *reinterpret_cast<float4*>(cterm + j) = *reinterpret_cast<const float4*>(a.cterm + (size_t)p * a.n + j);
+    } else
+    for (int j = threadIdx.x; j < a.n; j += 64 * W) {
         float2 q[16];
         float mx = -INFINITY, s = 0.f;
         for (int b0 = 0; b0 < a.rblocks; b0 += 16) {  // (16 partial loads in flight)
@@ -563,8 +600,8 @@ __global__ __launch_bounds__(64 * kDsWaves) void combine16_kernel(DsArgs a) {
     __syncthreads();
     const f16* sim = a.sim + (size_t)p * a.m * a.n;
     float* out = a.scores + (size_t)p * a.m * a.n;
-    const int r0 = rb * kDsRows + wave * (kDsRows / kDsWaves);
-    const int r1 = min(r0 + kDsRows / kDsWaves, a.m);
+    const int r0 = (rb * W + wave) * kDsBatch;
+    const int r1 = min(r0 + kDsBatch, a.m);
     for (int i0 = r0; i0 < r1; i0 += kDsBatch) {
         f16x8 x[kDsBatch][CPL];
         float rterm[kDsBatch];
@@ -789,10 +826,17 @@ int32_t lg_log_double_softmax(const float* sim, const float* z0, const float* z1
     return launched("lg_log_double_softmax");
 }
 
+namespace {
+// small launches (fewer than 64 blocks of 64 rows): 8-row one-wave blocks and a separate column pass
+bool ds_small(int32_t m, int32_t batch) { return (long)((m + kDsRows - 1) / kDsRows) * batch < 64; }
+int ds_rows(int32_t m, int32_t batch) { return ds_small(m, batch) ? kDsBatch : kDsRows; }
+}  // namespace
+
 size_t lg_log_double_softmax_f16_workspace(int32_t m, int32_t n, int32_t batch) {
     if (m <= 0 || n <= 0 || batch <= 0) return 0;
-    const size_t rb = (size_t)(m + kDsRows - 1) / kDsRows;
-    return ((size_t)batch * m * sizeof(float) + 255) / 256 * 256 + (size_t)batch * rb * n * sizeof(float2);
+    const size_t rb = (size_t)(m + ds_rows(m, batch) - 1) / ds_rows(m, batch);
+    return ((size_t)batch * m * sizeof(float) + 255) / 256 * 256 + ((size_t)batch * rb * n * sizeof(float2) + 255) / 256 * 256 +
+           (ds_small(m, batch) ? (size_t)batch * n * sizeof(float) : 0);
 }
 
 int32_t lg_log_double_softmax_f16(const void* sim, const void* z0, const void* z1, int64_t z_pair_stride,
@@ -806,14 +850,24 @@ int32_t lg_log_double_softmax_f16(const void* sim, const void* z0, const void* z
     if (m == 0 || n == 0 || batch == 0) return MHA_HD64_STATUS_SUCCESS;
     DsArgs a;
     a.sim = (const f16*)sim, a.z0 = (const f16*)z0, a.z1 = (const f16*)z1, a.zps = z_pair_stride, a.zrs = z_row_stride;
-    a.scores = scores, a.m = m, a.n = n, a.rblocks = (m + kDsRows - 1) / kDsRows;
+    const bool small = ds_small(m, batch);
+    const int rows = ds_rows(m, batch);
+    a.scores = scores, a.m = m, a.n = n, a.rblocks = (m + rows - 1) / rows;
     a.lse_row = reinterpret_cast<float*>(workspace);
-    a.col_part = reinterpret_cast<float2*>(reinterpret_cast<char*>(workspace) +
-                                           ((size_t)batch * m * sizeof(float) + 255) / 256 * 256);
+    const size_t lse_bytes = ((size_t)batch * m * sizeof(float) + 255) / 256 * 256;
+    a.col_part = reinterpret_cast<float2*>(reinterpret_cast<char*>(workspace) + lse_bytes);
+    a.cterm = reinterpret_cast<float*>(reinterpret_cast<char*>(workspace) + lse_bytes +
+                                       ((size_t)batch * a.rblocks * n * sizeof(float2) + 255) / 256 * 256);
     const dim3 grid(a.rblocks, batch);
-#define LG_DS(CPL)                                                                        \
-    hipLaunchKernelGGL((lse16_kernel<CPL>), grid, dim3(64 * kDsWaves), 0, stream, a);     \
-    hipLaunchKernelGGL((combine16_kernel<CPL>), grid, dim3(64 * kDsWaves), 0, stream, a);
+#define LG_DS(CPL)                                                                                       \
+    if (small) {                                                                                         \
+        hipLaunchKernelGGL((lse16_kernel<CPL, 1>), grid, dim3(64), 0, stream, a);                        \
+        hipLaunchKernelGGL(col_lse_kernel, dim3((n + 63) / 64, batch), dim3(64 * kColGroups), 0, stream, a); \
+        hipLaunchKernelGGL((combine16_kernel<CPL, 1, true>), grid, dim3(64), 0, stream, a);               \
+    } else {                                                                                             \
+        hipLaunchKernelGGL((lse16_kernel<CPL, kDsWaves>), grid, dim3(64 * kDsWaves), 0, stream, a);      \
+        hipLaunchKernelGGL((combine16_kernel<CPL, kDsWaves, false>), grid, dim3(64 * kDsWaves), 0, stream, a); \
+    }
     if (n <= 512) {
         LG_DS(1)
     } else if (n <= 1024) {
