@@ -602,12 +602,15 @@ def test_linear_cat_ln_gelu_matches_torch(pairs, n0, n1):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pairs,m,n", [(1, 64, 48), (3, 300, 256), (1, 130, 211), (16, 1024, 1024), (2, 2048, 2000)])
+@pytest.mark.parametrize("pairs,m,n", [(1, 64, 48), (3, 300, 256), (1, 130, 211), (16, 1024, 1024), (2, 2048, 2000),
+                                     (1, 2048, 2048), (1, 1003, 1016)])
 def test_fp16_head_and_inputs_kernels(pairs, m, n):
     """The fp16 forward's own kernels around the layers: lg_pair_inputs (pair-major x = the torch cat
     bit for bit; cos / sin = the fp16 FourierPositionalEncoding within one fp16 ulp) and
     lg_log_double_softmax_f16 (fp16 sim and strided fp16 matchability logits read directly) against
-    the torch restatement of lightglue.py:197-205 on the same fp16 inputs."""
+    the torch restatement of lightglue.py:197-205 on the same fp16 inputs — both of its launch
+    shapes: 64-row blocks (16 x 1024, 2 x 2048) and, below 64 of those, 8-row blocks with the
+    separate column pass (single pairs up to 2048 x 2048, three pairs of 300 rows)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from lightglue_amd import matcher as mt
