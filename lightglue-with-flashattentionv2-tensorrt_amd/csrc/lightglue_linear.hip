@@ -49,6 +49,12 @@ typedef __attribute__((address_space(3))) f16x8 lds_f16x8;
 #define LG_ABL 0
 #endif
 // (ablation build: -DLG_LN_ABL=1 drops the one-launch FFN kernel's normalisation and GELU)
+#ifndef LG_LN_KROT
+#define LG_LN_KROT 0
+#endif
+#ifndef LG_LN_AHOT
+#define LG_LN_AHOT 0
+#endif
 #ifndef LG_LN_ABL
 #define LG_LN_ABL 0
 #endif
@@ -698,15 +704,20 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
     last_ = t_entry_;
 #endif
 
-    auto src_of = [&](int t) { return tile_src<true, BK, NWP, NAP, 8>(p, (j0 + G * t) * MT, 0, wave, lane); };
+    // (diagnostic build -DLG_LN_AHOT=1: every tile's A operand DMA'd from rows 0.., L2-hot; wrong results)
+    auto src_of = [&](int t) { return tile_src<true, BK, NWP, NAP, 8>(p, LG_LN_AHOT ? 0 : (j0 + G * t) * MT, 0, wave, lane); };
     // the vectors into LDS (loaded ahead of the first stages, written after them: the compiler's wait
     // counts the DMA pieces), visible after the first step's barrier
     f16x8 pv = {};
     const f16* const pvs = tid < 64 ? p.bias : tid < 128 ? gamma : beta;
     if (tid < 192) pv = *reinterpret_cast<const f16x8*>(pvs + (tid & 63) * 8);
     TileSrc<NWP, NAP> cur = src_of(0);  // (the next tile's sources are computed where used: registers)
+    // (diagnostic build -DLG_LN_KROT=1: each workgroup walks K from its own offset, so the workgroups
+    // of an XCD do not all read the same W lines at once; the same sums in another order)
+    const int krot = LG_LN_KROT ? (int)(blockIdx.x & (KS - 1)) : 0;
+    auto kstep = [&](int k) { return (k + krot) & (KS - 1); };
 #pragma unroll
-    for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, 8>(cur, i, smem + i * SB, wave);
+    for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, 8>(cur, kstep(i), smem + i * SB, wave);
     if (tid < 192) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
 
     auto swz = [](int row) { return BK == 64 ? (row >> 1) & 7 : (row >> 2) & 3; };
@@ -751,8 +762,8 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
             LN_SEG(1);
             {
                 char* const fb = smem + (st == 0 ? NST - 1 : st - 1) * SB;
-                if (ks + NST - 1 < KS) tile_issue<true, BK, KS, NT, 8>(cur, ks + NST - 1, fb, wave);
-                else if (more) tile_issue<true, BK, KS, NT, 8>(src_of(t + 1), ks + NST - 1 - KS, fb, wave);
+                if (ks + NST - 1 < KS) tile_issue<true, BK, KS, NT, 8>(cur, kstep(ks + NST - 1), fb, wave);
+                else if (more) tile_issue<true, BK, KS, NT, 8>(src_of(t + 1), kstep(ks + NST - 1 - KS), fb, wave);
             }
             const unsigned sb = (unsigned)(st * SB);
             st_last = st;
