@@ -81,8 +81,8 @@ int32_t lg_linear_cat(const void* x, const void* ctx0, const void* ctx1, int32_t
 /* lg_linear_cat_ln_gelu: the FFN's first half (lightglue.py:101-106) after lg_linear_cat:
  *                       out [n0+n1, 512] = GELU(LayerNorm(fp16([x | merge_heads(ctx0, ctx1)] · Wᵀ + bias)))
  *                       with the LayerNorm's gamma, beta [512] and eps (exact-erf GELU). One launch
- *                       (128-row tiles owning whole rows) from a full round of its tiles on (m >= 32,768
- *                       rows; heads * 128 = 512, 16-B aligned bias / gamma / beta / out), else
+ *                       (tiles owning whole rows: 64-row tiles from m >= 16,384, 128-row tiles from
+ *                       m >= 32,768; heads * 128 = 512, 16-B aligned bias / gamma / beta / out), else
  *                       lg_linear_cat then lg_layernorm_gelu in place; see lg_linear_set_ln_fused. */
 int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
                               int32_t pairs, const void* w, const void* bias, const void* gamma, const void* beta,

@@ -666,12 +666,9 @@ __device__ unsigned long long g_ln_stamps[256 * 8 * 8];
     } while (0)
 #endif
 constexpr int kLnN = 512;
-// the one-launch form's tile: 128 rows, 32-deep K steps, 3 stages (A/B build -DLG_LN_MT=64: 64 rows,
-// 64-deep steps, 2 stages of 72 KiB, twice the tiles per workgroup)
-#ifndef LG_LN_MT
-#define LG_LN_MT 128
-#endif
-constexpr int kLnMT = LG_LN_MT, kLnBK = LG_LN_MT == 64 ? 64 : 32, kLnNST = LG_LN_MT == 64 ? 2 : 3;
+// the one-launch form's two tiles: 128 rows with 32-deep K steps through 3 stages of 40 KiB, and
+// 64 rows with 64-deep K steps through 2 stages of 72 KiB (twice the W bytes per row: it pays only
+// while the 128-row tiles would leave CUs idle; see lg_linear_cat_ln_gelu)
 template <int KS, int MT, int BK, int NST>
 __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16* __restrict__ gamma,
                                                            const f16* __restrict__ beta, float eps) {
@@ -893,13 +890,16 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
 }
 
 constexpr int kTileGrid = 256;  // the 256-row forms: one workgroup per CU
-// lg_linear_cat_ln_gelu's one-launch form (linear_ln_kernel): taken from one full round of its
-// 128-row tiles on (256: M >= 32,768 rows, P >= 16 pairs of 1024 keypoints). Measured against the two
-// launches (profiles/r05/ln_fused_by_size.jsonl): op alone 39.4 vs 42.3 us at P = 16, 72.7 vs 74.4 at
-// P = 32, but 32.2 vs 27.1 at P = 8 and 28.3 vs 9.2 at P = 1 (too few workgroups: each one's GELU vector
-// work runs after its GEMM with no other wave's MFMAs beside it); whole forwards P = 16 2.487 vs
-// 2.541 ms, P = 32 4.642 vs 4.701, P = 8 1.638 vs 1.497. lg_linear_set_ln_fused: 1 by size (default),
-// 0 always two launches, 2 always one (A/B).
+// lg_linear_cat_ln_gelu's one-launch form (linear_ln_kernel), by size: its 128-row tiles from one
+// full round of them on (256: M >= 32,768 rows, P >= 16 pairs of 1024 keypoints), its 64-row tiles
+// from a full round of those (256: M >= 16,384), two launches below. Measured against the two launches
+// (profiles/r05/ln_fused_by_size.jsonl, ln64_by_size.jsonl; op alone, us, two launches / 128-row /
+// 64-row): P = 1 9.2 / 28.3 / 16.8, P = 4 19.7 / 29.4 / 18.3, P = 8 27.1-27.7 / 32.2 / 21.9, P = 16
+// 42.2 / 36.3-39.4 / 38.4, P = 32 74.4-77.7 / 72.7 / 77.0 (few workgroups: each one's GELU vector work
+// runs after its GEMM with no other wave's MFMAs beside it; more rows per tile: fewer W bytes per
+// row); whole forwards P = 8 1.53-1.54 -> 1.45-1.47 ms (64-row), P = 16 2.541 -> 2.487 (128-row), P =
+// 32 4.701 -> 4.642, but P = 4 (half a round of 64-row tiles) 1.03-1.04 -> 1.05-1.06 (profiles/r05/
+// ln64_forms_forwards.txt). lg_linear_set_ln_fused: 1 by size (default), 0 always two launches, 2 always one.
 std::atomic<int> g_ln_fused{1};
 // The tile form (tile_form below): lg_linear_set_wide(0..3) or LG_LINEAR_WIDE forces one (where n
 // allows), for tests and A/B timing; -1 (the default) chooses by size.
@@ -1033,8 +1033,9 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
         !aligned8(bias) || !aligned8(out) || !(eps >= 0.f))
         return bad("lg_linear_cat_ln_gelu");
     if (m == 0) return MHA_HD64_STATUS_SUCCESS;
-    const int lnf = g_ln_fused.load();  // 1: from a full round of tiles on; 2: at every size (A/B)
-    const bool fused = lnf && n == kLnN && (lnf == 2 || (m + 127) / 128 >= kTileGrid) && aligned16(bias) && aligned16(gamma) &&
+    const int lnf = g_ln_fused.load();  // 1: by size; 2: at every size (A/B)
+    const bool big = (m + 127) / 128 >= kTileGrid;  // a full round of 128-row tiles
+    const bool fused = lnf && n == kLnN && (lnf == 2 || big || (m + 63) / 64 >= kTileGrid) && aligned16(bias) && aligned16(gamma) &&
                        aligned16(beta) && aligned16(out) && wide_mode() != 0;
     if (!fused) {  // the projection, then LayerNorm+GELU in place (lightglue_glue.hip)
         const int32_t st = lg_linear_cat(x, ctx0, ctx1, heads, n0, n1, pairs, w, bias, n, out, stream);
@@ -1045,11 +1046,15 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
     p.a = (const f16*)x, p.ctx0 = (const f16*)ctx0, p.ctx1 = (const f16*)ctx1, p.w = (const f16*)w;
     p.bias = (const f16*)bias, p.out[0] = (f16*)out;
     p.m = m, p.n = n, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
-    p.mtiles = (m + kLnMT - 1) / kLnMT;
+    p.mtiles = big ? (m + 127) / 128 : (m + 63) / 64;
     p.total = p.mtiles;
     const int grid = p.total < kTileGrid ? p.total : kTileGrid;
-    hipLaunchKernelGGL((linear_ln_kernel<512 / kLnBK, kLnMT, kLnBK, kLnNST>), dim3(grid), dim3(512), 0, stream, p,
-                       (const f16*)gamma, (const f16*)beta, eps);
+    if (big)
+        hipLaunchKernelGGL((linear_ln_kernel<512 / 32, 128, 32, 3>), dim3(grid), dim3(512), 0, stream, p,
+                           (const f16*)gamma, (const f16*)beta, eps);
+    else
+        hipLaunchKernelGGL((linear_ln_kernel<512 / 64, 64, 64, 2>), dim3(grid), dim3(512), 0, stream, p,
+                           (const f16*)gamma, (const f16*)beta, eps);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_linear_cat_ln_gelu",
