@@ -232,6 +232,23 @@ struct StreamScores {
     bool rs;        // some query of the wave exceeds the running max by > kRescaleThr (wave-uniform)
 };
 
+// Speculative running max (-DMHA_STREAM_SPEC=1: an A/B build, not shipped; round 5, VERDICT r04
+// item 2's "j2" step): an item's running max is its tile 0's and never moves, so the middle and
+// tail steps carry no row max of the next tile, no rescale decision and no rescale (≈ 20 of the
+// step's ≈ 44 non-exponential vector instructions). Exact while no later score exceeds it by
+// 2^16 (the fp16 P would overflow; below that fp16's relative precision does not depend on
+// magnitude and the row sums and O accumulate in fp32). An overflow makes the row sum +Inf (NaN
+// keys: NaN), which the epilogue sees: the item is marked, and at the end of the kernel the wave
+// recomputes its rows of every marked item with an exact online softmax (exact_item below). Measured
+// (profiles/r05/stream_spec_*): the step 1.04 -> 0.97 us, 32 calls 0.324 -> 0.342 of peak, 64 calls
+// 0.350 -> 0.370 on random inputs — but one key per head that beats tile 0's best by 2^16 (a
+// peaked attention row) sends one item per head down the rare path and the launch from 41 to 134
+// us, where the lazy-rescale form pays 1-4 %. A data-dependent 3x cliff is not a trade the default
+// kernel takes; the lazy form below stays the default.
+#ifndef MHA_STREAM_SPEC
+#define MHA_STREAM_SPEC 0
+#endif
+
 template <typename TOut, bool MULTI, int NW>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kernel(FwdArgs a) {
     constexpr int OSZ = (int)sizeof(TOut);
@@ -396,8 +413,17 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
             vfb[jj][ss] = cat8(tr_read(lds, v_addr1 + rowc), tr_read(lds, v_addr1 + rowc + 8 * 128));
         }
     };
+    // SPEC: the items (ordinal k of this workgroup's walk, bit min(k, 63)) with a row sum that
+    // overflowed (or a NaN key), recomputed exactly at the end
+    unsigned long long dirty = 0;
     // O = Oᵀ / l of an item (rows past nq: dropped by the descriptor)
-    auto epilogue = [&](__amdgpu_buffer_rsrc_t o_rs, int q0, unsigned qbad_it) {
+    auto epilogue = [&](__amdgpu_buffer_rsrc_t o_rs, int q0, unsigned qbad_it, int ord) {
+        if constexpr (MHA_STREAM_SPEC) {
+            unsigned lb;  // (the bits through an asm move: -fno-honor-nans folds a float class test)
+            asm volatile("v_mov_b32 %0, %1" : "=v"(lb) : "v"(l_acc[0]));
+            const bool over = (lb & 0x7f800000u) == 0x7f800000u && !((qbad_it >> r) & 1u);
+            if (__builtin_amdgcn_ballot_w64(over) != 0) dirty |= 1ull << (ord < 63 ? ord : 63);
+        }
         const float inv = inv_or_nan(l_acc[0], qbad_it, r);  // a non-finite query row: NaN
         const unsigned row = (unsigned)(q0 + 32 * wave + r);
         if constexpr (OSZ == 2) {
@@ -441,6 +467,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
     __amdgpu_buffer_rsrc_t prv_o = cur.o;
     int prv_q0 = 0;
     unsigned qbad_prv = 0;
+    int item_no = 0, prv_no = 0;  // ordinal of the current / previous item in this workgroup's walk
 
     // One step of the current item — every step is a full step of the pipeline: tile t's
     // exponentials; QKᵀ of global tile g + 1 (LAST: the next item's tile 0, with the next item's Q
@@ -463,6 +490,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         constexpr bool LAST = KIND == 3;
         constexpr bool MASK = KIND != 1 && KIND != 4;  // tile t + 1 may hold keys past nkv
         constexpr bool BAR = NW == 4 || KIND == 1 || KIND == 2 || KIND == 3;  // (NW 8: odd t)
+        // the row max of tile t + 1: every step of the lazy-rescale form; SPEC: the LAST step only
+        // (the next item's tile 0 sets its running max)
+        constexpr bool NEEDMAX = !MHA_STREAM_SPEC || LAST;
         const unsigned g = gb + (unsigned)t;
 #ifdef MHA_STREAM_PRIO_BAL
         // NW 8, between two barriers: the first step at raised priority, the second at normal, so
@@ -489,7 +519,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         // online-softmax decision for tile t (rare): the max moves now for tiles t, t + 1, ...;
         // O and l follow after tile t − 1's P·V (at the old max) is in
         float alpha = 1.f;
-        const bool rescale = !FIRST && c.rs;
+        const bool rescale = !MHA_STREAM_SPEC && !FIRST && c.rs;
         if (rescale) {
             asm volatile("" ::: "memory");  // (a real branch)
             const float d = fmaxf(c.mx, 0.f);
@@ -545,7 +575,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         auto fill = [&](int gi) {
             if (gi < 16) exp_pair(gi);
             if (gi >= 4 && gi < 20) cvt(gi - 4);
-            if (gi >= 14 && gi < 18) maxk(gi - 14);
+            if (NEEDMAX && gi >= 14 && gi < 18) maxk(gi - 14);
         };
 
         constexpr int SB = KIND == 0 ? 2 : (KIND == 1 || KIND == 4) ? 6 : KIND == 3 ? 16 : 10;  // (stamps)
@@ -604,11 +634,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
             if (lim < kTileKV) {  // (wave-uniform, rare: a partial or padding tile)
                 asm volatile("" ::: "memory");
                 mask_tile(n, lim);
-                mt[0] = mt[1] = mt[2] = mt[3] = tree_max(n.s0, n.s1);
+                if constexpr (NEEDMAX) mt[0] = mt[1] = mt[2] = mt[3] = tree_max(n.s0, n.s1);
             }
         }
-        n.mx = xhalf_max(fmaxf(max3f(mt[0], mt[1], mt[2]), mt[3]));
-        if constexpr (!LAST) n.rs = __builtin_amdgcn_ballot_w64(n.mx > kRescaleThr) != 0;
+        if constexpr (NEEDMAX) n.mx = xhalf_max(fmaxf(max3f(mt[0], mt[1], mt[2]), mt[3]));
+        if constexpr (!LAST && !MHA_STREAM_SPEC) n.rs = __builtin_amdgcn_ballot_w64(n.mx > kRescaleThr) != 0;
         if (rescale) {  // tile t − 1's P·V went in at the old max: O and l follow the new one
             asm volatile("" ::: "memory");
             o0 *= alpha;
@@ -616,7 +646,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
             l_acc *= alpha;
         }
         if constexpr (FIRST) {  // the previous item is complete: its output, then a fresh O and l
-            if (prev) epilogue(prv_o, prv_q0, qbad_prv);
+            if (prev) epilogue(prv_o, prv_q0, qbad_prv, prv_no);
             o0 = f32x16{};
             o1 = f32x16{};
             l_acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -735,6 +765,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         prv_o = cur.o;
         prv_q0 = cur.q0;
         qbad_prv = qbad;
+        prv_no = item_no++;
         prev = true;
         // ---- next item ----
         j += G;
@@ -745,6 +776,74 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         const bool more = j + G < je;
         nxt = stream_item<MULTI, OSZ, NW>(a, more ? j + G : j, more);
     }
+    // SPEC's rare path: this wave's 32 rows of item jj, exactly — a running max per 64-key tile
+    // (exact online softmax, rescale at every move), the step's MFMA forms with their operands
+    // loaded from global memory: K fragments as read_k reads the ring (key row r / r + 32, chunk
+    // 2s + hh), Vᵀ fragments element by element (lane (dim, k-group g) holds V[key][dim] for the 8
+    // keys that P's pack (jj, ss) puts at k = 8g .. 8g + 7), then the item's epilogue.
+    auto exact_item = [&](int jj) {
+        const StreamItem it = stream_item<MULTI, OSZ, NW>(a, jj, true);
+        const StreamLoader kv = stream_kv<MULTI>(a, jj, true);
+        const unsigned qrow = (unsigned)(it.q0 + 32 * wave + r);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            qf[s] = stream_scale_q(__builtin_bit_cast(
+                f16x8, __builtin_amdgcn_raw_buffer_load_b128(it.q, qrow * 128u + (unsigned)(2 * s + hh) * 16u, 0, 0)));
+        const unsigned qb = q_nonfinite_fix(qf);
+        float m = -INFINITY, l = 0.f;
+        o0 = f32x16{};
+        o1 = f32x16{};
+        const int ntl = (it.nkv + kTileKV - 1) / kTileKV;
+        for (int t = 0; t < ntl; ++t) {
+            const unsigned kt = (unsigned)(t * kTileKV);
+            StreamScores sc;
+            const f32x16 zero = {};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb) {
+                    const f16x8 kfr = __builtin_bit_cast(
+                        f16x8, __builtin_amdgcn_raw_buffer_load_b128(kv.k, (kt + (unsigned)(32 * kb + r)) * 128u + (unsigned)(2 * s + hh) * 16u, 0, 0));
+                    f32x16& acc = kb ? sc.s1 : sc.s0;
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kfr, qf[s], s == 0 ? zero : acc, 0, 0, 0);
+                }
+            }
+            if (it.nkv - (int)kt < kTileKV) mask_tile(sc, it.nkv - (int)kt);
+            const float mn = fmaxf(m, xhalf_max(tree_max(sc.s0, sc.s1)));
+            const float alpha = __builtin_amdgcn_exp2f(m - mn);  // (the first tile: exp2(-Inf) = 0)
+            m = mn;
+            float ls = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                sc.s0[i] = __builtin_amdgcn_exp2f(sc.s0[i] - m);
+                sc.s1[i] = __builtin_amdgcn_exp2f(sc.s1[i] - m);
+                ls += sc.s0[i] + sc.s1[i];
+            }
+            const auto lsw = __builtin_amdgcn_permlane32_swap(__float_as_uint(ls), __float_as_uint(ls), false, false);
+            l = l * alpha + (__uint_as_float(lsw[0]) + __uint_as_float(lsw[1]));  // (own half + the other)
+            o0 *= alpha;
+            o1 *= alpha;
+#pragma unroll
+            for (int pj = 0; pj < 2; ++pj)
+#pragma unroll
+                for (int ps = 0; ps < 2; ++ps) {
+                    const f32x16& x = pj ? sc.s1 : sc.s0;
+                    f16x8 pk, va, vb;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        pk[e] = (f16)x[8 * ps + e];
+                        const int i = 8 * ps + e;
+                        const unsigned key = kt + (unsigned)((i & 3) + 8 * (i >> 2) + 4 * hh + 32 * pj);
+                        va[e] = __builtin_bit_cast(f16, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(kv.v, key * 128u + (unsigned)r * 2u, 0, 0));
+                        vb[e] = __builtin_bit_cast(f16, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(kv.v, key * 128u + (unsigned)(32 + r) * 2u, 0, 0));
+                    }
+                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pk, o0, 0, 0, 0);
+                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vb, pk, o1, 0, 0, 0);
+                }
+        }
+        l_acc = f32x4{l, l, l, l};
+        epilogue(it.o, it.q0, qb, 63);
+    };
     // flush: the last item's last tile (P in pB, V in its slot: no refill has reached it)
     {
         const unsigned vb_t = ((gb + (unsigned)cur.nt - 1u) & kSM) * (unsigned)kSSlot;
@@ -757,10 +856,19 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
             o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb[jj][ss], pB[jj][ss], o1, 0, 0, 0);
             l_acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a_sum, pB[jj][ss], l_acc, 0, 0, 0);
         }
-        epilogue(prv_o, prv_q0, qbad_prv);
+        epilogue(prv_o, prv_q0, qbad_prv, prv_no);
     }
     // drain: the loader's trailing (empty) pieces and the output stores
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (MHA_STREAM_SPEC) {
+        if (dirty) {  // (wave-uniform, rare) the exact rows of the marked items, over their stores
+            asm volatile("" ::: "memory");
+            const int j_first = jb + loc;
+            for (int k = 0; j_first + k * G < je; ++k)
+                if ((dirty >> (k < 63 ? k : 63)) & 1ull) exact_item(j_first + k * G);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
 #ifdef MHA_STREAM_STAMPS
     unsigned long long ck_exit[2];
     asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(ck_exit[0]), "=s"(ck_exit[1])::"memory");

@@ -53,7 +53,7 @@ def _ref(q, k, v):
     return torch.softmax(q @ k.transpose(-1, -2) / 8.0, dim=-1) @ v
 
 
-def _check(got, ref, scale, tag):
+def _check(got, ref, scale, tag, v):
     got64 = got.double()
     assert torch.isfinite(got64).all(), tag
     d = (got64 - ref).abs()
@@ -62,6 +62,10 @@ def _check(got, ref, scale, tag):
         bound = REG_ABS * scale + ref.abs() * 2.0 ** -11
     else:
         bound = torch.full_like(ref, REG_ABS * scale)
+    # fewer than one 64-key tile: the fp16 rounding of each P (2^-11 relative) no longer averages
+    # out over many keys, so a row's error reaches 2^-11 max|v - o| (observed 1.6e-3 at nkv = 2)
+    if v.shape[2] < 64:
+        bound = bound + 2.0 ** -10 * float(v.double().abs().max())
     excess = float((d - bound).max())
     assert excess <= 0, (tag, f"regression excess {excess:.3e}, max-abs {float(d.max()):.3e}")
 
@@ -78,7 +82,7 @@ def test_fuzz_plugin_enqueue(seed, dev):
     o = mha_hd64(q, k, v)
     torch.cuda.synchronize()
     assert o.dtype == dt and o.shape == q.shape
-    _check(o, _ref(q.half(), k.half(), v.half()), scale, ("plugin", seed, nq, nkv, dt))
+    _check(o, _ref(q.half(), k.half(), v.half()), scale, ("plugin", seed, nq, nkv, dt), v)
 
 
 @pytest.mark.parametrize("seed", range(64))
@@ -98,7 +102,7 @@ def test_fuzz_batched_launcher(seed, dev):
     o = mha_hd64_batched(q, k, v, out_dtype=out_dt)
     torch.cuda.synchronize()
     assert o.dtype == out_dt and o.shape == q.shape
-    _check(o, _ref(q.half(), k.half(), v.half()), scale, ("batched", seed, b, nq, nkv, in_dt, out_dt))
+    _check(o, _ref(q.half(), k.half(), v.half()), scale, ("batched", seed, b, nq, nkv, in_dt, out_dt), v)
 
 
 @pytest.mark.parametrize("seed", range(48))
@@ -123,4 +127,4 @@ def test_fuzz_grouped_launcher(seed, dev):
     assert len(outs) == ncall
     for i, ((q, k, v), o, s) in enumerate(zip(calls, outs, scales)):
         assert o.dtype == out_dt and o.shape == q.shape, (seed, i)
-        _check(o, _ref(q.half(), k.half(), v.half()), s, ("grouped", seed, i, tuple(q.shape), tuple(k.shape)))
+        _check(o, _ref(q.half(), k.half(), v.half()), s, ("grouped", seed, i, tuple(q.shape), tuple(k.shape)), v)
