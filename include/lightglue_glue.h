@@ -87,6 +87,16 @@ int32_t lg_linear_cat(const void* x, const void* ctx0, const void* ctx1, int32_t
 int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
                               int32_t pairs, const void* w, const void* bias, const void* gamma, const void* beta,
                               float eps, void* out, hipStream_t stream);
+/* lg_linear_cat_ffn:    the whole FFN with the block's residual (lightglue.py:101-106, 150-151 / 174-175):
+ *                       out [n0+n1, d] = x + fp16(W2 · GELU(LayerNorm(W1 · [x | merge_heads(ctx0, ctx1)] + b1)) + b2)
+ *                       with d = heads*64 = 256, W1 [2d, 2d], W2 [d, 2d]: lg_linear_cat_ln_gelu into h [m, 2d]
+ *                       then lg_linear(h, W2, b2, res = x); with lg_linear_set_ffn_fused(1), one launch
+ *                       (ffn_kernel: the GELU output stays in LDS) where lg_linear_cat_ln_gelu takes its
+ *                       128-row one-launch form (m >= 32,768, or lg_linear_set_ln_fused(2)), bitwise equal.
+ *                       h must hold m*2d fp16 either way; out must not alias x (16-B aligned pointers). */
+int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
+                          int32_t pairs, const void* w1, const void* b1, const void* gamma, const void* beta, float eps,
+                          const void* w2, const void* b2, void* h, void* out, hipStream_t stream);
 /* lg_linear_qkv_rotary: SelfBlock projection (lightglue.py:111-134) with W's rows and the bias in
  *                       [q|k|v][head][dim] order (row j*heads*64 + h*64 + d = Wqkv row (h*64+d)*3 + j):
  *                       rotary (cos/sin [n0+n1, 64]) on q and k in fp16 arithmetic, as the reference's
@@ -139,6 +149,10 @@ int32_t lg_linear_set_wide(int32_t mode);
  * round of its tiles on, 0 always two launches, 2 always one launch (A/B). The forms agree within fp16
  * rounding, not in every bit (the one-launch variance is two-pass). Returns the previous setting. */
 int32_t lg_linear_set_ln_fused(int32_t on);
+/* Test and benchmark hook for lg_linear_cat_ffn: 0 (the default) its two calls, 1 its one launch
+ * wherever lg_linear_cat_ln_gelu takes its 128-row one-launch form (measured slower: an A/B path).
+ * Returns the previous value. */
+int32_t lg_linear_set_ffn_fused(int32_t on);
 
 #ifdef __cplusplus
 }

@@ -889,6 +889,291 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
 #endif
 }
 
+
+// ---- the whole FFN with its residual in one launch (lg_linear_cat_ffn) ----
+// out = x + W2·GELU(LN(W1·[x | heads] + b1)) + b2 (lightglue.py:101-106 and the blocks' residual,
+// :150-151 / :174-175). Phase 1 is linear_ln_kernel<16, 128, 32, 3> (128-row tiles owning whole
+// rows); its fp16 GELU output h stays in LDS (128 KiB, [row][512] with 16-B chunks XOR-swizzled by
+// row & 7: conflict-free fragment reads) instead of going to HBM and back. Phase 2: 8 waves as 2 (m)
+// x 4 (n) tiles of 64 x 64 of the 128 x 256 output, K = 512 in 16-deep MFMA steps whose W2
+// fragments come from global memory (256 KiB, L2-resident) straight into registers kFfnPf steps
+// ahead; then fp16(acc + b2) + x, staged through LDS and stored as whole 128-B row segments — the
+// operations of lg_linear_cat_ln_gelu + lg_linear(res = x) in the same order (bitwise equal). Each
+// tile starts its ring afresh (the next tile's first K steps would land in LDS that h occupies).
+// (ablation builds, -DLG_FFN_ABL=bits, wrong results: 1 no W2 loads in phase 2, 2 no phase-2 MFMAs,
+// 4 no phase-2 epilogue (residual loads, stores), 8 no phase 2 at all)
+#ifndef LG_FFN_ABL
+#define LG_FFN_ABL 0
+#endif
+constexpr int kFfnOut = 256;  // the FFN's output channels (d)
+#ifndef LG_FFN_PF
+#define LG_FFN_PF 8
+#endif
+constexpr int kFfnPf = LG_FFN_PF;  // W2 fragment steps in flight per wave (A/B: -DLG_FFN_PF)
+__global__ __launch_bounds__(512, 1) void ffn_kernel(LinArgs p, const f16* __restrict__ gamma, const f16* __restrict__ beta,
+                                                     float eps, const f16* __restrict__ w2, const f16* __restrict__ b2) {
+    constexpr int KS = 16, MT = 128, BK = 32, NST = 3, NT = kLnN;
+    constexpr int WM = 2, WN = 4, WTN = NT / WN, NB = WTN / 32, NP = WTN / 64;
+    constexpr int SB = (MT + NT) * BK * 2;                             // 40 KiB ring stages
+    constexpr int NWP = NT * BK * 2 / 8192, NAP = MT * BK * 2 / 8192;  // 4 + 1 pieces per wave and step
+    constexpr int D = NWP + NAP;
+    constexpr int kH = 0;                         // h [128][512] fp16 (over the ring, after phase 1)
+    constexpr int kPar = MT * NT * 2;             // b1, gamma, beta [512] fp16
+    constexpr int kRed = kPar + 3 * NT * 2;       // row partials [2][MT][WN] fp32
+    static_assert(NST * SB <= kPar && (NST - 2) * D <= 63, "shape");
+    __shared__ __attribute__((aligned(16))) char smem[kRed + 2 * MT * WN * 4];
+    lds_char* const lds = (lds_char*)smem;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WM, wn = wave / WM;
+    const int r = lane & 31, hh = lane >> 5;
+    const int T = p.total, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int q8 = T >> 3, r8 = T & 7;
+    const int jb = xcd * q8 + min(xcd, r8), je = jb + q8 + (xcd < r8 ? 1 : 0);
+    const int G = ((int)gridDim.x - xcd + 7) >> 3;
+    const int j0 = jb + loc;
+    if (j0 >= je) return;
+    const int ntile_w = (je - j0 + G - 1) / G;
+
+    auto src_of = [&](int t) { return tile_src<true, BK, NWP, NAP, 8>(p, (j0 + G * t) * MT, 0, wave, lane); };
+    f16x8 pv = {};
+    const f16* const pvs = tid < 64 ? p.bias : tid < 128 ? gamma : beta;
+    if (tid < 192) pv = *reinterpret_cast<const f16x8*>(pvs + (tid & 63) * 8);
+    TileSrc<NWP, NAP> cur = src_of(0);
+#pragma unroll
+    for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, 8>(cur, i, smem + i * SB, wave);
+    if (tid < 192) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
+
+    auto swz = [](int row) { return (row >> 2) & 3; };
+    unsigned wro[NB], aro[2];
+    int wsw[NB], asw[2];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int wrow = wn * WTN + 32 * b + r;
+        wro[b] = (unsigned)(wrow * BK * 2), wsw[b] = swz(wrow);
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int arow = wm * 64 + 32 * b + r;
+        aro[b] = (unsigned)(NT * BK * 2 + arow * BK * 2), asw[b] = swz(arow);
+    }
+    const int cr = lane >> 3, cc = lane & 7;
+    float* const red = (float*)(void*)(smem + kRed);  // [pass][row][wn]
+    auto red_sum = [&](int off) {
+        float v = 0.f;
+#pragma unroll
+        for (int q = 0; q < WN; q += 4) {
+            const f32x4 w4 = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (off + q) * 4);
+            v += (w4[0] + w4[1]) + (w4[2] + w4[3]);
+        }
+        return v;
+    };
+    // phase 2's W2 fragments: lane (r, hh) of n-block nb reads row wn * 64 + 32 nb + r, k 16 j + 8 hh
+    // (a buffer descriptor: one lane offset, the step's offset a scalar constant)
+    const __amdgpu_buffer_rsrc_t w2rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(w2), (short)0, kFfnOut * NT * 2, 0x00020000);
+    const unsigned w2lo = (unsigned)(((wn * 64 + r) * NT + 8 * hh) * 2);
+    auto w2frag = [&](int nb, int j) {
+        if constexpr (LG_FFN_ABL & 1) {
+            unsigned z0, z1, z2, z3, src = w2lo + (unsigned)j;
+            asm volatile("v_mov_b32 %0, %4\n\tv_mov_b32 %1, %4\n\tv_mov_b32 %2, %4\n\tv_mov_b32 %3, %4"
+                         : "=v"(z0), "=v"(z1), "=v"(z2), "=v"(z3) : "v"(src));
+            typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+            return __builtin_bit_cast(f16x8, u32x4_{z0, z1, z2, z3 + (unsigned)nb});
+        }
+        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(w2rs, w2lo, (32 * nb * NT + 16 * j) * 2, 0));
+    };
+    for (int t = 0; t < ntile_w; ++t) {
+        const int m0 = (j0 + G * t) * MT;
+        if (t > 0) {  // a fresh ring (the previous tile's output stores drained first: exact counts)
+            cur = src_of(t);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, 8>(cur, i, smem + i * SB, wave);
+        }
+        f32x16 acc[NB][2] = {};
+        int st = 0;
+#pragma unroll 2
+        for (int ks = 0; ks < KS; ++ks) {
+            if (ks + NST - 2 > KS - 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * D) : "memory");
+            __builtin_amdgcn_s_barrier();
+            if (ks + NST - 1 < KS) tile_issue<true, BK, KS, NT, 8>(cur, ks + NST - 1, smem + (st == 0 ? NST - 1 : st - 1) * SB, wave);
+            const unsigned sb = (unsigned)(st * SB);
+            st = st == NST - 1 ? 0 : st + 1;
+#pragma unroll
+            for (int s = 0; s < BK / 16; ++s) {
+                const int u = 2 * s + hh;
+                f16x8 wf[NB], af[2];
+#pragma unroll
+                for (int b = 0; b < NB; ++b) wf[b] = *(lds_f16x8*)(lds + sb + wro[b] + ((u ^ wsw[b]) << 4));
+#pragma unroll
+                for (int b = 0; b < 2; ++b) af[b] = *(lds_f16x8*)(lds + sb + aro[b] + ((u ^ asw[b]) << 4));
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+                    for (int mb = 0; mb < 2; ++mb)
+                        acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[nb], af[mb], acc[nb][mb], 0, 0, 0);
+            }
+        }
+        // ---- h = GELU(LN(fp16(acc + b1))) as linear_ln_kernel computes it, into the h region ----
+        const int nw0 = wn * WTN;
+        float rs[2];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            float s = 0.f;
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const u32x2 b4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + (nw0 + 32 * nb + 8 * g + 4 * hh) * 2);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float a = acc[nb][mb][4 * g + u];
+                        const float h = (u & 1) ? mixh<1>(a, b4[u >> 1]) : mixh<0>(a, b4[u >> 1]);
+                        acc[nb][mb][4 * g + u] = h;
+                        s += h;
+                    }
+                }
+            rs[mb] = s + __shfl_xor(s, 32, 64);
+        }
+        if (hh == 0) {
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) red[(wm * 64 + 32 * mb + r) * WN + wn] = rs[mb];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        float mean[2];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            mean[mb] = red_sum((wm * 64 + 32 * mb + r) * WN) * (1.f / kLnN);
+            float q = 0.f;
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const float d = acc[nb][mb][e] - mean[mb];
+                    acc[nb][mb][e] = d;
+                    q = __builtin_fmaf(d, d, q);
+                }
+            rs[mb] = q + __shfl_xor(q, 32, 64);
+        }
+        if (hh == 0) {
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) red[MT * WN + (wm * 64 + 32 * mb + r) * WN + wn] = rs[mb];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // (also: every wave is done reading the ring, which h overwrites)
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+            const int row = wm * 64 + 32 * mb + r;  // tile row of this lane
+            const float rstd = __builtin_amdgcn_rsqf(red_sum(MT * WN + row * WN) * (1.f / kLnN) + eps);
+#pragma unroll
+            for (int np = 0; np < NP; ++np)
+#pragma unroll
+                for (int nbl = 0; nbl < 2; ++nbl)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int n = nw0 + 64 * np + 32 * nbl + 8 * g + 4 * hh;
+                        const u32x2 g4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + NT * 2 + n * 2);
+                        const u32x2 b4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + 2 * NT * 2 + n * 2);
+                        f16x4 o;
+#pragma unroll
+                        for (int u = 0; u < 4; u += 2) {
+                            const f32x16& av = acc[2 * np + nbl][mb];
+                            const f32x2 xr = f32x2{av[4 * g + u], av[4 * g + u + 1]} * rstd;
+                            const f32x2 gl = gelu_as2(f32x2{mixf<0>(xr[0], g4[u >> 1], b4[u >> 1]), mixf<1>(xr[1], g4[u >> 1], b4[u >> 1])});
+                            o[u] = (f16)gl[0];
+                            o[u + 1] = (f16)gl[1];
+                        }
+                        *(__attribute__((address_space(3))) f16x4*)(lds + kH + row * (NT * 2) + (((n >> 3) ^ (row & 7)) << 4) + 8 * hh) = o;
+                    }
+        }
+        // the first W2 fragments in flight across the barrier (the phase-1 accumulators are dead here)
+        f16x8 wq[kFfnPf][2];
+#pragma unroll
+        for (int j = 0; j < kFfnPf; ++j)
+#pragma unroll
+            for (int nb = 0; nb < 2; ++nb) wq[j][nb] = w2frag(nb, j);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // h complete
+        if constexpr (LG_FFN_ABL & 8) continue;
+        // ---- phase 2: out tile [wm * 64, +64) x [wn * 64, +64) = h · W2ᵀ, K in 16-deep steps ----
+        f32x16 o2[2][2] = {};
+#pragma unroll 1
+        for (int jb2 = 0; jb2 < KS * 2; jb2 += kFfnPf)
+#pragma unroll
+        for (int jj = 0; jj < kFfnPf; ++jj) {
+            const int j = jb2 + jj;
+            const f16x8 w0 = wq[jj][0], w1 = wq[jj][1];
+            if (j + kFfnPf < KS * 2) {
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) wq[jj][nb] = w2frag(nb, j + kFfnPf);
+            }
+            f16x8 hf[2];
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) {
+                const int row = wm * 64 + 32 * mb + r;
+                hf[mb] = *(lds_f16x8*)(lds + kH + row * (NT * 2) + (((2 * j + hh) ^ (row & 7)) << 4));
+            }
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) {
+                if constexpr (LG_FFN_ABL & 2) {
+                    asm volatile("" ::"v"(w0), "v"(w1), "v"(hf[mb]));
+                    continue;
+                }
+                o2[0][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w0, hf[mb], o2[0][mb], 0, 0, 0);
+                o2[1][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w1, hf[mb], o2[1][mb], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave is done reading h: its region stages the output
+        if constexpr (LG_FFN_ABL & 4) {
+            asm volatile("" ::"v"(o2[0][0]), "v"(o2[0][1]), "v"(o2[1][0]), "v"(o2[1][1]));
+            continue;
+        }
+        // ---- out = fp16(fp16(acc + b2) + x): 32 rows x 64 channels a round through this wave's 4 KiB ----
+        lds_char* const stg = lds + kH + wave * 4096;
+        const int c0 = wn * 64;
+        u32x2 bb[2][4];
+#pragma unroll
+        for (int nbl = 0; nbl < 2; ++nbl)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) bb[nbl][g] = *reinterpret_cast<const u32x2*>(b2 + c0 + 32 * nbl + 8 * g + 4 * hh);
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+            for (int nbl = 0; nbl < 2; ++nbl)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x16& a = o2[nbl][mb];
+                    const f16x4 b4 = __builtin_bit_cast(f16x4, bb[nbl][g]);
+                    const f16x4 v = f16x4{lin_val(a[4 * g], b4[0]), lin_val(a[4 * g + 1], b4[1]),
+                                          lin_val(a[4 * g + 2], b4[2]), lin_val(a[4 * g + 3], b4[3])};
+                    *(__attribute__((address_space(3))) f16x4*)(stg + r * 128 + (((4 * nbl + g) ^ (r & 7)) << 4) + 8 * hh) = v;
+                }
+            f16x8 o[4], xr[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int rl = 8 * i + cr;
+                o[i] = *(lds_f16x8*)(stg + rl * 128 + ((cc ^ (rl & 7)) << 4));
+                const int row = min(m0 + wm * 64 + 32 * mb + rl, p.m - 1);
+                xr[i] = *reinterpret_cast<const f16x8*>(p.a + (size_t)row * (p.k / 2) + c0 + 8 * cc);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = min(m0 + wm * 64 + 32 * mb + 8 * i + cr, p.m - 1);
+                f16x8 v = o[i];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], xr[i][e]);
+                st_out(p.out[0] + (size_t)row * kFfnOut + c0 + 8 * cc, v);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the next round rewrites stg)
+        }
+        __builtin_amdgcn_s_barrier();  // (the next tile's ring overwrites the staging regions)
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 constexpr int kTileGrid = 256;  // the 256-row forms: one workgroup per CU
 // lg_linear_cat_ln_gelu's one-launch form (linear_ln_kernel), by size: its 128-row tiles from one
 // full round of them on (256: M >= 32,768 rows, P >= 16 pairs of 1024 keypoints), its 64-row tiles
@@ -901,6 +1186,13 @@ constexpr int kTileGrid = 256;  // the 256-row forms: one workgroup per CU
 // 32 4.701 -> 4.642, but P = 4 (half a round of 64-row tiles) 1.03-1.04 -> 1.05-1.06 (profiles/r05/
 // ln64_forms_forwards.txt). lg_linear_set_ln_fused: 1 by size (default), 0 always two launches, 2 always one.
 std::atomic<int> g_ln_fused{1};
+// lg_linear_cat_ffn's one-launch form (ffn_kernel) wherever lg_linear_cat_ln_gelu takes its 128-row
+// one-launch form (1) or never (0, the default: its two calls). Measured (profiles/r05/ffn_one_launch_ab.jsonl,
+// ffn_ablations.jsonl): 55.98 vs 52.68 us at P = 16 and forwards 1-3 % slower — phase 2 re-reads W2
+// per 128-row tile (4x the W bytes per row of lg_linear's 256 x 128 tiles: 7.5 us of L2 -> CU traffic),
+// and its epilogue (residual loads, the 16.8 MB store burst, 7.6 us) overlaps nothing with one tile per
+// workgroup, which costs more than h's HBM round trip saves. Kept as an A/B path (lg_linear_set_ffn_fused).
+std::atomic<int> g_ffn_fused{0};
 // The tile form (tile_form below): lg_linear_set_wide(0..3) or LG_LINEAR_WIDE forces one (where n
 // allows), for tests and A/B timing; -1 (the default) chooses by size.
 std::atomic<int> g_wide{-2};
@@ -1061,6 +1353,38 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
                                                     hipGetErrorString(e));
 }
 
+int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
+                          int32_t pairs, const void* w1, const void* b1, const void* gamma, const void* beta, float eps,
+                          const void* w2, const void* b2, void* h, void* out, hipStream_t stream) {
+    const int d = heads * kD, k = 2 * d, m = pairs * (n0 + n1);
+    if (heads <= 0 || n0 < 0 || n1 < 0 || pairs < 0 || !shape_ok(m, k, k) || !x || !w1 || !b1 || !gamma || !beta || !w2 ||
+        !b2 || !h || !out || out == x || !aligned16(x) || (n0 && !aligned16(ctx0)) || (n1 && !aligned16(ctx1)) ||
+        !aligned16(w1) || !aligned16(w2) || !aligned8(b1) || !aligned8(b2) || !aligned16(h) || !aligned8(out) || !(eps >= 0.f))
+        return bad("lg_linear_cat_ffn");
+    if (m == 0) return MHA_HD64_STATUS_SUCCESS;
+    const int lnf = g_ln_fused.load();  // as lg_linear_cat_ln_gelu: 1 by size, 2 at every size, 0 never
+    const bool big = (m + 127) / 128 >= kTileGrid;
+    const bool fused = lnf && g_ffn_fused.load() && k == kLnN && d == kFfnOut && (lnf == 2 || big) && aligned16(b1) && aligned16(gamma) &&
+                       aligned16(beta) && aligned16(b2) && aligned16(out) && wide_mode() != 0;
+    if (!fused) {  // h in the caller's buffer, then the output projection with the residual
+        const int32_t st = lg_linear_cat_ln_gelu(x, ctx0, ctx1, heads, n0, n1, pairs, w1, b1, gamma, beta, eps, h, stream);
+        if (st != MHA_HD64_STATUS_SUCCESS) return st;
+        return lg_linear(h, w2, b2, x, m, d, k, out, stream);
+    }
+    LinArgs p{};
+    p.a = (const f16*)x, p.ctx0 = (const f16*)ctx0, p.ctx1 = (const f16*)ctx1, p.w = (const f16*)w1;
+    p.bias = (const f16*)b1, p.out[0] = (f16*)out;
+    p.m = m, p.n = k, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
+    p.mtiles = (m + 127) / 128;
+    p.total = p.mtiles;
+    const int grid = p.total < kTileGrid ? p.total : kTileGrid;
+    hipLaunchKernelGGL(ffn_kernel, dim3(grid), dim3(512), 0, stream, p, (const f16*)gamma, (const f16*)beta, eps,
+                       (const f16*)w2, (const f16*)b2);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
+                           : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_linear_cat_ffn", hipGetErrorString(e));
+}
+
 int32_t lg_linear_qkv_rotary(const void* x, const void* w_perm, const void* b_perm, const void* cosv,
                              const void* sinv, int32_t heads, int32_t n0, int32_t n1, int32_t pairs, int32_t k,
                              void* q0, void* k0, void* v0, void* q1, void* k1, void* v1, hipStream_t stream) {
@@ -1106,5 +1430,6 @@ int32_t lg_diag_ln_stamps(void* host_dst) {  // (diagnostic build only: not in t
 }
 #endif
 int32_t lg_linear_set_ln_fused(int32_t on) { return g_ln_fused.exchange(on == 2 ? 2 : on ? 1 : 0); }
+int32_t lg_linear_set_ffn_fused(int32_t on) { return g_ffn_fused.exchange(on ? 1 : 0); }
 
 }  // extern "C"

@@ -133,6 +133,7 @@ SIGNATURES.update({
     "lg_linear": ([_P, _P, _P, _P, _I, _I, _I, _P, _P], _I),
     "lg_linear_cat": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P, _P], _I),
     "lg_linear_cat_ln_gelu": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, ctypes.c_float, _P, _P], _I),
+    "lg_linear_cat_ffn": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, ctypes.c_float, _P, _P, _P, _P, _P], _I),
     "lg_linear_qkv_rotary": ([_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P], _I),
     "lg_linear_split2": ([_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P], _I),
     "lg_layernorm_gelu": ([_I, _P, _P, _P, _I, _I, ctypes.c_float, _P, _P], _I),
@@ -144,6 +145,7 @@ SIGNATURES.update({
     "lg_log_double_softmax_f16": ([_P, _P, _P, ctypes.c_int64, ctypes.c_int64, _I, _I, _I, _P, _P, _P], _I),
     "lg_pair_inputs": ([_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P], _I),
     "lg_linear_set_ln_fused": ([_I], _I),
+    "lg_linear_set_ffn_fused": ([_I], _I),
     # kernel-form switches (include/mha_hd64.h "kernel-form switches")
     "mha_hd64_set_fused_combine": ([_I], None),
     "mha_hd64_set_f32_inkernel": ([_I], None),

@@ -122,6 +122,22 @@ class _Hip:
         return out
 
     @staticmethod
+    def ffn(x, c0, c1, w, b, ln: nn.LayerNorm, w2, b2):
+        """x + ffn([x | merge_heads(c0, c1)]) (lightglue.py:101-106 with the block's residual):
+        linear_cat_ln_gelu into a scratch h, then linear(h, w2, b2, res=x) — or, with
+        lg_linear_set_ffn_fused(1), one launch (bitwise the same; measured slower, an A/B path)."""
+        pr, heads, n0, n1 = c0.shape[0], c0.shape[1], c0.shape[2], c1.shape[2]
+        m = pr * (n0 + n1)
+        h = torch.empty((1, m, w.shape[0]), dtype=x.dtype, device=x.device)
+        out = torch.empty((1, m, w2.shape[0]), dtype=x.dtype, device=x.device)
+        st = _lib.load().lg_linear_cat_ffn(x.data_ptr(), c0.data_ptr(), c1.data_ptr(), heads, n0, n1, pr,
+                                           w.data_ptr(), b.data_ptr(), ln.weight.data_ptr(), ln.bias.data_ptr(),
+                                           float(ln.eps), w2.data_ptr(), b2.data_ptr(), h.data_ptr(), out.data_ptr(),
+                                           _Hip._stream(x))
+        _check(st, "lg_linear_cat_ffn")
+        return out
+
+    @staticmethod
     def linear_cat_ln_gelu(x, c0, c1, w, b, ln: nn.LayerNorm):
         """GELU(LayerNorm([x | merge_heads(c0, c1)]·wᵀ + b)) in one launch (P pairs of equal sizes)."""
         pr, heads, n0, n1 = c0.shape[0], c0.shape[1], c0.shape[2], c1.shape[2]
@@ -401,24 +417,22 @@ class TransformerLayer(nn.Module):
 
 
     def _forward_fused(self, x, cos, sin, splits, attention: AttnFn):
-        """fp16 hip path: 4 launches per block -- projection(+rotary/head split), grouped
+        """fp16 hip path: 4 launches per block -- projection (+rotary/head split), grouped
         attention, FFN input projection gathering [x | heads] (message projection folded in) with
-        LayerNorm+GELU in its epilogue, FFN output projection + residual."""
+        LayerNorm+GELU in its epilogue, FFN output projection + residual (lg_linear_cat_ffn)."""
         sa, ca = self.self_attn, self.cross_attn
         wq, bq = _qkv_perm(sa, x.dtype)
         qkv = _Hip.linear_qkv_rotary(x, wq, bq, cos, sin, sa.heads, splits)
         c0, c1 = attention(qkv)                                          # self0, self1: one launch
         w0, b0 = _ffn_in_fused(sa, sa.out_proj, x.dtype)
-        h = _Hip.linear_cat_ln_gelu(x, c0, c1, w0, b0, sa.ffn[1])
-        x = _Hip.linear(h, sa.ffn[3].weight, sa.ffn[3].bias, res=x)
+        x = _Hip.ffn(x, c0, c1, w0, b0, sa.ffn[1], sa.ffn[3].weight, sa.ffn[3].bias)
         wc, bc = _cached(ca, "_qkv_stacked", (ca.to_qk.weight, ca.to_qk.bias, ca.to_v.weight, ca.to_v.bias),
                          x.dtype, lambda: (torch.cat((ca.to_qk.weight, ca.to_v.weight), 0),
                                            torch.cat((ca.to_qk.bias, ca.to_v.bias), 0)))
         (qk0, qk1), (v0, v1) = _Hip.linear_split2(x, wc, bc, ca.heads, splits)
         m0, m1 = attention([(qk0, qk1, v1), (qk1, qk0, v0)])            # cross: one launch
         w0, b0 = _ffn_in_fused(ca, ca.to_out, x.dtype)
-        h = _Hip.linear_cat_ln_gelu(x, m0, m1, w0, b0, ca.ffn[1])
-        return _Hip.linear(h, ca.ffn[3].weight, ca.ffn[3].bias, res=x)
+        return _Hip.ffn(x, m0, m1, w0, b0, ca.ffn[1], ca.ffn[3].weight, ca.ffn[3].bias)
 
 
 def log_double_softmax(sim: torch.Tensor, z0: torch.Tensor, z1: torch.Tensor) -> torch.Tensor:

@@ -602,6 +602,66 @@ def test_linear_cat_ln_gelu_matches_torch(pairs, n0, n1):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pairs,n0,n1", [(16, 1024, 1024), (32, 1024, 1024), (17, 1000, 977), (1, 300, 257), (2, 64, 1)])
+def test_linear_cat_ffn_equals_two_calls(pairs, n0, n1):
+    """lg_linear_cat_ffn (the whole FFN with the residual, lightglue.py:101-106 + :150-151) against
+    the two calls it makes by default: lg_linear_cat_ln_gelu then lg_linear(h, W2, b2, res = x). Its
+    one-launch form (lg_linear_set_ffn_fused(1): ffn_kernel, the GELU output kept in LDS, the second
+    GEMM's W2 fragments from global memory) runs the same operations in the same order, so the outputs
+    are bitwise equal: at lg_linear_cat_ln_gelu's choice (one launch from 32,768 rows: P = 16 / 32;
+    two calls below), the one-launch form forced at
+    every size (lg_linear_set_ln_fused(2): ragged m, a partial last tile, 2 tiles per workgroup at
+    P = 32; below 32,768 rows against the 64-row form of the first half: a few ulps), and the
+    two-call form forced (0)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lightglue_amd import _lib
+    from lightglue_amd import matcher as mt
+
+    dev, dt, h = torch.device("cuda:0"), torch.float16, 4
+    lib = _lib.load()
+    gen = torch.Generator().manual_seed(11 + pairs)
+    rnd = lambda *s: torch.randn(*s, generator=gen).to(dev, dt)  # noqa: E731
+    with torch.no_grad():
+        x = rnd(1, pairs * (n0 + n1), 256) * 0.5
+        c0, c1 = rnd(pairs, h, n0, 64), rnd(pairs, h, n1, 64)
+        w, b = rnd(512, 512) * 0.05, rnd(512) * 0.1
+        w2, b2 = rnd(256, 512) * 0.05, rnd(256) * 0.1
+        ln = torch.nn.LayerNorm(512).to(dev, dt)
+        ln.weight.copy_(1 + 0.1 * rnd(512))
+        ln.bias.copy_(0.1 * rnd(512))
+        outs = {}
+        hh = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)
+        default = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2)  # two calls (lg_linear_set_ffn_fused(0))
+        two = mt._Hip.linear(hh, w2, b2, res=x)
+        prev_f = lib.lg_linear_set_ffn_fused(1)
+        try:
+            for mode in (1, 2, 0):
+                prev = lib.lg_linear_set_ln_fused(mode)
+                try:
+                    outs[mode] = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2)
+                    hh = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)
+                    outs[(mode, "two")] = mt._Hip.linear(hh, w2, b2, res=x)
+                finally:
+                    lib.lg_linear_set_ln_fused(prev)
+        finally:
+            lib.lg_linear_set_ffn_fused(prev_f)
+        torch.cuda.synchronize()
+    assert torch.equal(default, two)
+    big = pairs * (n0 + n1) >= 256 * 128
+    for mode in (1, 2, 0):
+        assert torch.isfinite(outs[mode]).all(), mode
+        d = float((outs[mode].float() - outs[(mode, "two")].float()).abs().max())
+        if mode == 2 and not big:
+            # (forced below 32,768 rows, lg_linear_cat_ln_gelu takes its 64-row tiles, whose row
+            # statistics sum 8 partials where the 128-row tiles of ffn_kernel sum 4: h can differ
+            # by an ulp, the output by a few)
+            assert d <= 4e-3, (mode, d)
+        else:
+            assert torch.equal(outs[mode], outs[(mode, "two")]), (mode, d)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("pairs,m,n", [(1, 64, 48), (3, 300, 256), (1, 130, 211), (16, 1024, 1024), (2, 2048, 2000),
                                      (1, 2048, 2048), (1, 1003, 1016)])
 def test_fp16_head_and_inputs_kernels(pairs, m, n):
