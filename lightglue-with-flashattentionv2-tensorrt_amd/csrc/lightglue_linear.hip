@@ -392,16 +392,16 @@ __device__ __forceinline__ void tile_issue(const TileSrc<NWP, NAP>& t, int ks, c
 // count them (every lane stores; rows past m are computed on the clamped last A row and write that
 // row's own bytes again, so the count is exact).
 // RES (EPI_BIAS): p.res is added (a compile-time form: its prefetch holds registers).
-template <int EPI, bool GATHER, bool RES, int KS, int MT, int NT, int BK, int NST>
-__global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
-    constexpr int WM = MT / 64, WN = 8 / WM, WTN = NT / WN, NB = WTN / 32, NP = WTN / 64;
+template <int EPI, bool GATHER, bool RES, int KS, int MT, int NT, int BK, int NST, int NWV = 8>
+__global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void linear_tile_kernel(LinArgs p) {
+    constexpr int WM = MT / 64, WN = NWV / WM, WTN = NT / WN, NB = WTN / 32, NP = WTN / 64;
     constexpr int SB = (MT + NT) * BK * 2;                               // one ring stage
-    constexpr int NWP = NT * BK * 2 / 8192, NAP = MT * BK * 2 / 8192;    // 1-KiB DMA pieces per wave, step
+    constexpr int NWP = NT * BK * 2 / (NWV * 1024), NAP = MT * BK * 2 / (NWV * 1024);  // 1-KiB DMA pieces per wave, step
     constexpr int D = NWP + NAP;
     constexpr int SPW = 2 * NP * 4;                                      // output stores per wave and tile
     // epilogue operands loaded per wave and tile (at its first K step): bias, residual / cos + sin rows
     constexpr int PF = NB * 4 + (RES ? 2 * NP * 4 : 0) + (EPI == EPI_QKV_ROTARY ? 16 : 0);
-    static_assert(SB >= 8 * 4096, "a staging region per wave inside one ring stage");
+    static_assert(SB >= NWV * 4096, "a staging region per wave inside one ring stage");
     static_assert(KS >= NST - 1 && NB % 2 == 0 && (NST - 2) * D + SPW + PF <= 63, "shape");
     static_assert(NB == 2 || (EPI != EPI_QKV_ROTARY && !RES), "64 x 128 wave tiles: no room for the prefetched tables");
     __shared__ __attribute__((aligned(16))) char smem[NST * SB];
@@ -422,12 +422,12 @@ __global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
 
     auto src_of = [&](int t) {
         const int jt = j0 + G * t, mt = jt / ntiles;
-        return tile_src<GATHER, BK, NWP, NAP, 8>(p, mt * MT, (jt - mt * ntiles) * NT, wave, lane);
+        return tile_src<GATHER, BK, NWP, NAP, NWV>(p, mt * MT, (jt - mt * ntiles) * NT, wave, lane);
     };
     TileSrc<NWP, NAP> cur = src_of(0), nxt = cur;
 #pragma unroll
     for (int i = 0; i < NST - 1; ++i)
-        if constexpr (!(LG_ABL & 4)) tile_issue<GATHER, BK, KS, NT, 8>(cur, i, smem + i * SB, wave);
+        if constexpr (!(LG_ABL & 4)) tile_issue<GATHER, BK, KS, NT, NWV>(cur, i, smem + i * SB, wave);
 
     // fragment rows of this lane: W rows wn * WTN + 32 b + r, A rows wm * 64 + 32 b + r
     auto swz = [](int row) { return BK == 64 ? (row >> 1) & 7 : (row >> 2) & 3; };
@@ -503,8 +503,8 @@ __global__ __launch_bounds__(512, 1) void linear_tile_kernel(LinArgs p) {
             {
                 char* const fb = smem + (st == 0 ? NST - 1 : st - 1) * SB;
                 if (LG_ABL & 4) {
-                } else if (ks + NST - 1 < KS) tile_issue<GATHER, BK, KS, NT, 8>(cur, ks + NST - 1, fb, wave);
-                else if (more) tile_issue<GATHER, BK, KS, NT, 8>(nxt, ks + NST - 1 - KS, fb, wave);
+                } else if (ks + NST - 1 < KS) tile_issue<GATHER, BK, KS, NT, NWV>(cur, ks + NST - 1, fb, wave);
+                else if (more) tile_issue<GATHER, BK, KS, NT, NWV>(nxt, ks + NST - 1 - KS, fb, wave);
             }
             const unsigned sb = (unsigned)(st * SB);
             st_last = st;
@@ -1204,7 +1204,7 @@ int wide_mode() {
         if (e && *e) {
             char* end = nullptr;
             const long x = std::strtol(e, &end, 10);
-            if (end != e) m = x < -1 ? -1 : (x > 3 ? 3 : x);
+            if (end != e) m = x < -1 ? -1 : (x > 5 ? 5 : x);
         }
         int expect = -2;
         g_wide.compare_exchange_strong(expect, (int)m);
@@ -1217,11 +1217,16 @@ bool aligned8(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 7) == 0;
 
 // The 256-row tile forms (linear_tile_kernel): 1 = 256 x 128, 2 = 256 x 256 (32-deep K steps, 4
 // stages; plain EPI_BIAS only: the residual / rotary tables and the scatter addressing do not fit
-// beside its accumulators), 3 = 128 x 256. Forced by lg_linear_set_wide / LG_LINEAR_WIDE where n and the operand
-// alignment allow, else chosen by size: 256 x 128 tiles from half a round (128) of them on (at
-// P = 4 pairs, M = 8,192: qkv 12.5 vs 20.2 us, cat 11.5 vs 19.0, split2 / linear even; below, the
-// 64 x 64 form's more workgroups win; profiles/r05/linear_ab_tile_forms.jsonl).
-int tile_form(const LinArgs& p, int epi) {
+// beside its accumulators), 3 = 128 x 256; 4 / 5 = 128 x 128 on 4 waves, two workgroups per CU
+// (64-deep K steps through 2 stages / 32-deep through 4). Form 4 against form 1 (profiles/r05/
+// tile_form4_ab.jsonl, us): qkv 18.5 / 26.6 / 48.8 -> 15.9 / 25.1 / 46.5 at P = 8 / 16 / 32, split2
+// 17.5 -> 17.0 and linear+res 12.2 / 16.9 / 30.7 -> 9.8 / 16.6 / 28.5 (form 1 leaves half the CUs idle
+// at P = 8), cat 14.5 / 24.6 / 45.1 -> 14.8 / 24.3 / 46.0; at P = 4 qkv 10.9 = 10.9, split2 8.6 -> 7.4,
+// linear+res 10.5 (64 x 64) -> 8.1, cat 11.5 -> 9.3; whole forwards P = 4 / 8 / 16 +2.3 / +2.9 / +0.8 %,
+// P = 32 -1.0 % (form_fwd_ab.jsonl): the default below; forms 1-3 (the round's earlier default was form 1
+// from half a round of its tiles) stay for lg_linear_set_wide / LG_LINEAR_WIDE, which force a form where
+// n and the operand alignment allow.
+int tile_form(const LinArgs& p, int epi, bool gather) {
     bool al = aligned16(p.bias);
     const int nout = epi == EPI_BIAS ? 1 : epi == EPI_QKV_ROTARY ? 6 : 4;
     for (int i = 0; i < nout; ++i) al = al && aligned16(p.out[i]);
@@ -1232,35 +1237,42 @@ int tile_form(const LinArgs& p, int epi) {
     // (and it steps through the rows of a tile with one wrap at most: pairs of more than 56 rows)
     if (epi != EPI_BIAS && ((long long)p.m * p.heads * kD >= (1LL << 32) || p.n0 + p.n1 <= 56)) return 0;
     const int w = wide_mode();
-    const int f = w >= 0 ? w : ((long)((p.m + 255) / 256) * (p.n / 128) >= 128 ? 1 : 0);
+    // by size: the 4-wave 128 x 128 form (two workgroups per CU) from 128 of its tiles on, else the
+    // 64 x 64 form (profiles/r05/tile_form4_ab.jsonl: at 128 tiles form 4 wins linear+res at P = 4 and
+    // lg_linear_cat at P = 2, loses split2 at P = 2 by 1 us; from 192 tiles on it wins or ties every op
+    // but lg_linear_cat at P = 32, 2 % behind 256 x 128, which the matcher does not call there)
+    (void)gather;
+    const int f = w >= 0 ? w : ((long)((p.m + 127) / 128) * (p.n / 128) >= 128 ? 4 : 0);
     if (f == 1 && p.n % 128 == 0) return 1;
     if (f == 2 && p.n % 256 == 0) return (p.res || epi != EPI_BIAS) ? 1 : 2;
     if (f == 3 && p.n % 256 == 0) return 3;
+    if (f >= 4 && p.n % 128 == 0) return f;
     return f >= 1 && p.n % 128 == 0 ? 1 : 0;
 }
 
-template <int EPI, bool GATHER, bool RES, int MT, int NT, int BK, int NST>
+template <int EPI, bool GATHER, bool RES, int MT, int NT, int BK, int NST, int NWV>
 void launch_tile_r(LinArgs& p, hipStream_t stream) {
     p.mtiles = (p.m + MT - 1) / MT;
     p.total = p.mtiles * (p.n / NT);
-    const int grid = p.total < kTileGrid ? p.total : kTileGrid;  // persistent: one round
+    constexpr int cap = kTileGrid * 8 / NWV;  // persistent: one round (4 waves: two workgroups per CU)
+    const int grid = p.total < cap ? p.total : cap;
     if (p.k == 256)
-        hipLaunchKernelGGL((linear_tile_kernel<EPI, GATHER, RES, 256 / BK, MT, NT, BK, NST>), dim3(grid), dim3(512), 0, stream, p);
+        hipLaunchKernelGGL((linear_tile_kernel<EPI, GATHER, RES, 256 / BK, MT, NT, BK, NST, NWV>), dim3(grid), dim3(64 * NWV), 0, stream, p);
     else
-        hipLaunchKernelGGL((linear_tile_kernel<EPI, GATHER, RES, 512 / BK, MT, NT, BK, NST>), dim3(grid), dim3(512), 0, stream, p);
+        hipLaunchKernelGGL((linear_tile_kernel<EPI, GATHER, RES, 512 / BK, MT, NT, BK, NST, NWV>), dim3(grid), dim3(64 * NWV), 0, stream, p);
 }
-template <int EPI, bool GATHER, int MT, int NT, int BK, int NST>
+template <int EPI, bool GATHER, int MT, int NT, int BK, int NST, int NWV = 8>
 void launch_tile(LinArgs& p, hipStream_t stream) {
-    constexpr bool WIDE_WAVE = NT * MT / 64 / 8 / 32 > 2;  // 64 x 128 wave tiles
+    constexpr bool WIDE_WAVE = NT * MT / 64 / NWV / 32 > 2;  // 64 x 128 wave tiles
     if constexpr (EPI == EPI_BIAS && !GATHER && !WIDE_WAVE) {
-        if (p.res) return launch_tile_r<EPI, GATHER, true, MT, NT, BK, NST>(p, stream);
+        if (p.res) return launch_tile_r<EPI, GATHER, true, MT, NT, BK, NST, NWV>(p, stream);
     }
-    if constexpr (!(WIDE_WAVE && EPI == EPI_QKV_ROTARY)) launch_tile_r<EPI, GATHER, false, MT, NT, BK, NST>(p, stream);
+    if constexpr (!(WIDE_WAVE && EPI == EPI_QKV_ROTARY)) launch_tile_r<EPI, GATHER, false, MT, NT, BK, NST, NWV>(p, stream);
 }
 
 template <int EPI, bool GATHER>
 int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
-    int form = tile_form(p, EPI);
+    int form = tile_form(p, EPI, GATHER);
     if (GATHER && form == 2) form = 1;  // (the gather's per-piece sources do not fit beside 64 x 128 wave tiles)
     switch (form) {
         case 1: launch_tile<EPI, GATHER, 256, 128, 64, 3>(p, stream); break;
@@ -1268,6 +1280,8 @@ int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
             if constexpr (!GATHER && EPI == EPI_BIAS) launch_tile<EPI, GATHER, 256, 256, 32, 4>(p, stream);
             break;
         case 3: launch_tile<EPI, GATHER, 128, 256, 64, 3>(p, stream); break;
+        case 4: launch_tile<EPI, GATHER, 128, 128, 64, 2, 4>(p, stream); break;
+        case 5: launch_tile<EPI, GATHER, 128, 128, 32, 4, 4>(p, stream); break;
         default:
             p.mtiles = (p.m + kBM - 1) / kBM;
             p.total = p.mtiles * (p.n / kBN);
@@ -1419,7 +1433,7 @@ int32_t lg_linear_split2(const void* x, const void* w, const void* bias, int32_t
 
 int32_t lg_linear_set_wide(int32_t mode) {
     wide_mode();
-    return g_wide.exchange(mode < 0 ? -1 : (mode > 3 ? 3 : mode));
+    return g_wide.exchange(mode < 0 ? -1 : (mode > 5 ? 5 : mode));
 }
 
 int32_t lg_glue_abi_version(void) { return LG_GLUE_ABI_VERSION; }

@@ -541,7 +541,7 @@ def test_wide_projections_equal_narrow(pairs, n0, n1):
         try:
             narrow = [flat(o) for o in run()]
             forms = []
-            for mode in (1, 2, 3):  # 256 x 128; 256 x 256 (32-deep K steps); 128 x 256
+            for mode in (1, 2, 3, 4, 5):  # 256 x 128; 256 x 256 (32-deep K steps); 128 x 256; 128 x 128 (4 waves)
                 lib.lg_linear_set_wide(mode)
                 forms.append([flat(o) for o in run()])
             torch.cuda.synchronize()

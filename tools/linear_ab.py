@@ -1,5 +1,6 @@
 """Diagnostic: the matcher projections (include/lightglue_glue.h lg_linear*) in their 64 x 64 and
-256 x 128-tile and 256 x 256-tile forms (lg_linear_set_wide 0 / 1 / 2) at P image pairs of n keypoints per image, graph
+256 x 128-tile, 256 x 256-tile, 128 x 256-tile and 128 x 128-tile 4-wave forms (lg_linear_set_wide
+0 / 1 / 2 / 3 / 4-5) at P image pairs of n keypoints per image, graph
 replay of back-to-back launches, interleaved; TFLOP/s of each.
 
     python tools/linear_ab.py [P] [n] [op substring] [modes, e.g. 012] [b]
@@ -108,7 +109,9 @@ def main():
         row = {"op": name, "M": M}
         for wide in modes:
             us = statistics.median(times[(name, wide)])
-            row[("narrow", "wide", "square", "square5")[wide]] = {"us": round(us, 2), "tflops": round(2.0 * M * kn / us / 1e6, 1)}
+            # (files before round 5's forms 4 / 5 labelled forms 1 / 2 / 3 "wide" / "square" / "square5")
+            row[("narrow", "wide", "square", "square5", "t128x128_4w", "t128x128_4w_bk32")[wide]] = {
+                "us": round(us, 2), "tflops": round(2.0 * M * kn / us / 1e6, 1)}
         row["alg_MB"] = round(nbytes[name] / 1e6, 2)
         if yard:
             us = statistics.median(times[(name, "blas")])
