@@ -141,7 +141,7 @@ int32_t lg_pair_inputs(const void* desc0, const void* desc1, const void* kpts0, 
  * pairs per forward): 0 the 64 x 64 form only, 1 the 256 x 128 form where n allows, 2 the
  * 256 x 256 form where n allows (plain bias outputs; else 1), 3 the 128 x 256 form (A/B only),
  * 4 the 128 x 128 form on 4 waves (two workgroups per CU; the by-size choice from 128 of its
- * tiles on), 5 the same with 32-deep K steps (A/B only), -1 (the default) chosen by size; values
+ * tiles and 8,192 rows on), 5 the same with 32-deep K steps (A/B only), -1 (the default) chosen by size; values
  * outside -1..5 are clamped. The environment variable
  * LG_LINEAR_WIDE sets the initial mode the same way. Every form gives the same bits. Returns the
  * previous mode. */

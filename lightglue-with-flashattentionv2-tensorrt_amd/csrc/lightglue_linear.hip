@@ -1237,12 +1237,14 @@ int tile_form(const LinArgs& p, int epi, bool gather) {
     // (and it steps through the rows of a tile with one wrap at most: pairs of more than 56 rows)
     if (epi != EPI_BIAS && ((long long)p.m * p.heads * kD >= (1LL << 32) || p.n0 + p.n1 <= 56)) return 0;
     const int w = wide_mode();
-    // by size: the 4-wave 128 x 128 form (two workgroups per CU) from 128 of its tiles on, else the
-    // 64 x 64 form (profiles/r05/tile_form4_ab.jsonl: at 128 tiles form 4 wins linear+res at P = 4 and
-    // lg_linear_cat at P = 2, loses split2 at P = 2 by 1 us; from 192 tiles on it wins or ties every op
-    // but lg_linear_cat at P = 32, 2 % behind 256 x 128, which the matcher does not call there)
+    // by size: the 4-wave 128 x 128 form (two workgroups per CU) from 128 of its tiles and 8,192 rows
+    // on, else the 64 x 64 form (profiles/r05/tile_form4_ab.jsonl: at 128 tiles form 4 wins
+    // linear+res at P = 4 and lg_linear_cat at P = 2, loses split2 at P = 2 by 1 us; from 192 tiles on
+    // it wins or ties every op but lg_linear_cat at P = 32, 2 % behind 256 x 128, which the matcher
+    // does not call there. Whole forwards (form_fwd_ab_final.jsonl): P = 2 (4,096 rows) 2 % faster
+    // with the 64 x 64 form everywhere, P = 4 / 8 / 16 7 / 3 / 1 % faster than form 1 with this rule)
     (void)gather;
-    const int f = w >= 0 ? w : ((long)((p.m + 127) / 128) * (p.n / 128) >= 128 ? 4 : 0);
+    const int f = w >= 0 ? w : (p.m >= 8192 && (long)((p.m + 127) / 128) * (p.n / 128) >= 128 ? 4 : 0);
     if (f == 1 && p.n % 128 == 0) return 1;
     if (f == 2 && p.n % 256 == 0) return (p.res || epi != EPI_BIAS) ? 1 : 2;
     if (f == 3 && p.n % 256 == 0) return 3;
