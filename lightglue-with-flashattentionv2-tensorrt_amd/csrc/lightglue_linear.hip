@@ -666,16 +666,19 @@ __device__ unsigned long long g_ln_stamps[256 * 8 * 8];
     } while (0)
 #endif
 constexpr int kLnN = 512;
+#ifndef LG_LN_2WG
+#define LG_LN_2WG 0
+#endif
 // the one-launch form's two tiles: 128 rows with 32-deep K steps through 3 stages of 40 KiB, and
 // 64 rows with 64-deep K steps through 2 stages of 72 KiB (twice the W bytes per row: it pays only
 // while the 128-row tiles would leave CUs idle; see lg_linear_cat_ln_gelu)
-template <int KS, int MT, int BK, int NST>
-__global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16* __restrict__ gamma,
-                                                           const f16* __restrict__ beta, float eps) {
+template <int KS, int MT, int BK, int NST, int NWV = 8>
+__global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void linear_ln_kernel(LinArgs p, const f16* __restrict__ gamma,
+                                                                              const f16* __restrict__ beta, float eps) {
     constexpr int NT = kLnN;
-    constexpr int WM = MT / 64, WN = 8 / WM, WTN = NT / WN, NB = WTN / 32, NP = WTN / 64;
+    constexpr int WM = MT / 64, WN = NWV / WM, WTN = NT / WN, NB = WTN / 32, NP = WTN / 64;
     constexpr int SB = (MT + NT) * BK * 2;                             // 40 KiB
-    constexpr int NWP = NT * BK * 2 / 8192, NAP = MT * BK * 2 / 8192;  // 4 + 1 pieces per wave and step
+    constexpr int NWP = NT * BK * 2 / (NWV * 1024), NAP = MT * BK * 2 / (NWV * 1024);  // pieces per wave and step
     constexpr int D = NWP + NAP;
     constexpr int SPW = 2 * NP * 4;
     constexpr int kPar = NST * SB;                  // vectors: bias, gamma, beta [512] fp16
@@ -702,7 +705,7 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
 #endif
 
     // (diagnostic build -DLG_LN_AHOT=1: every tile's A operand DMA'd from rows 0.., L2-hot; wrong results)
-    auto src_of = [&](int t) { return tile_src<true, BK, NWP, NAP, 8>(p, LG_LN_AHOT ? 0 : (j0 + G * t) * MT, 0, wave, lane); };
+    auto src_of = [&](int t) { return tile_src<true, BK, NWP, NAP, NWV>(p, LG_LN_AHOT ? 0 : (j0 + G * t) * MT, 0, wave, lane); };
     // the vectors into LDS (loaded ahead of the first stages, written after them: the compiler's wait
     // counts the DMA pieces), visible after the first step's barrier
     f16x8 pv = {};
@@ -714,7 +717,7 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
     const int krot = LG_LN_KROT ? (int)(blockIdx.x & (KS - 1)) : 0;
     auto kstep = [&](int k) { return (k + krot) & (KS - 1); };
 #pragma unroll
-    for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, 8>(cur, kstep(i), smem + i * SB, wave);
+    for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, NWV>(cur, kstep(i), smem + i * SB, wave);
     if (tid < 192) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
 
     auto swz = [](int row) { return BK == 64 ? (row >> 1) & 7 : (row >> 2) & 3; };
@@ -759,8 +762,8 @@ __global__ __launch_bounds__(512, 1) void linear_ln_kernel(LinArgs p, const f16*
             LN_SEG(1);
             {
                 char* const fb = smem + (st == 0 ? NST - 1 : st - 1) * SB;
-                if (ks + NST - 1 < KS) tile_issue<true, BK, KS, NT, 8>(cur, kstep(ks + NST - 1), fb, wave);
-                else if (more) tile_issue<true, BK, KS, NT, 8>(src_of(t + 1), kstep(ks + NST - 1 - KS), fb, wave);
+                if (ks + NST - 1 < KS) tile_issue<true, BK, KS, NT, NWV>(cur, kstep(ks + NST - 1), fb, wave);
+                else if (more) tile_issue<true, BK, KS, NT, NWV>(src_of(t + 1), kstep(ks + NST - 1 - KS), fb, wave);
             }
             const unsigned sb = (unsigned)(st * SB);
             st_last = st;
@@ -1357,7 +1360,13 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
     p.mtiles = big ? (m + 127) / 128 : (m + 63) / 64;
     p.total = p.mtiles;
     const int grid = p.total < kTileGrid ? p.total : kTileGrid;
-    if (big)
+    if (big && LG_LN_2WG) {  // (A/B build: 64-row tiles on 4 waves, two workgroups per CU)
+        p.mtiles = (m + 63) / 64;
+        p.total = p.mtiles;
+        const int g2 = p.total < 2 * kTileGrid ? p.total : 2 * kTileGrid;
+        hipLaunchKernelGGL((linear_ln_kernel<512 / 32, 64, 32, 2, 4>), dim3(g2), dim3(256), 0, stream, p,
+                           (const f16*)gamma, (const f16*)beta, eps);
+    } else if (big)
         hipLaunchKernelGGL((linear_ln_kernel<512 / 32, 128, 32, 3>), dim3(grid), dim3(512), 0, stream, p,
                            (const f16*)gamma, (const f16*)beta, eps);
     else
