@@ -493,7 +493,7 @@ def test_torch_glue_runs_pairs_one_by_one():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pairs,n0,n1", [(3, 37, 70), (2, 1000, 777), (16, 1024, 1024), (40, 20, 30), (5, 1, 63),
+@pytest.mark.parametrize("pairs,n0,n1", [(3, 37, 70), (2, 1000, 777), (16, 1024, 1024), (9, 1000, 1011), (40, 20, 30), (5, 1, 63),
                                          (4, 56, 1)])
 def test_wide_projections_equal_narrow(pairs, n0, n1):
     """The projections' 256-row tile forms (csrc/lightglue_linear.hip linear_tile_kernel: 256 x 128,
