@@ -64,7 +64,8 @@ int32_t lg_merge_heads_cat(int32_t dtype, const void* x, const void* x0, const v
                            int32_t n1, int32_t pairs, void* out, hipStream_t stream);
 
 /* FFN middle (lightglue.py:101-106): y = GELU(LayerNorm(x) * gamma + beta), exact (erf) GELU,
- * x, y [rows, dim], dim a multiple of 64 and <= 1024. */
+ * x, y [rows, dim], dim a multiple of 64 and <= 1024; y == x (in place) is allowed: each row is read
+ * whole before any of it is written. */
 int32_t lg_layernorm_gelu(int32_t dtype, const void* x, const void* gamma, const void* beta, int32_t rows,
                           int32_t dim, float eps, void* y, hipStream_t stream);
 

@@ -136,7 +136,7 @@ __device__ __forceinline__ float wave_max(float x) {
 
 // ---- LayerNorm + exact GELU (one wave per row, dim / 64 values per lane) ----
 template <typename T, int PER>
-__global__ __launch_bounds__(256) void ln_gelu_kernel(const T* __restrict__ x, const T* __restrict__ g,
+__global__ __launch_bounds__(256) void ln_gelu_kernel(const T* x, const T* __restrict__ g,
                                                       const T* __restrict__ bta, int rows, float eps, T* y) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -203,7 +203,7 @@ __device__ __forceinline__ f32x2 gelu_as2(f32x2 x) {
 
 // fp16, dim 512 (the matcher's FFN width): a lane owns 8 contiguous columns (one 16-B load of x,
 // gamma and beta), sum and sum of squares reduced together (fp32, E[x^2] - mean^2).
-__global__ __launch_bounds__(256) void ln_gelu_512_f16_kernel(const f16* __restrict__ x, const f16* __restrict__ g,
+__global__ __launch_bounds__(256) void ln_gelu_512_f16_kernel(const f16* x, const f16* __restrict__ g,
                                                               const f16* __restrict__ bta, int rows, float eps,
                                                               f16* y) {
     typedef f16 f16x8 __attribute__((ext_vector_type(8)));
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256) void ln_gelu_512_f16_kernel(const f16* __restr
 #endif
 constexpr int kLnDepth = LG_LN_DEPTH;  // rows in flight per wave beyond the one computed
 constexpr int kLnBlocksPerCU = LG_LN_BPC;
-__global__ __launch_bounds__(256) void ln_gelu_512_rows_kernel(const f16* __restrict__ x, const f16* __restrict__ g,
+__global__ __launch_bounds__(256) void ln_gelu_512_rows_kernel(const f16* x, const f16* __restrict__ g,
                                                                const f16* __restrict__ bta, int rows, float eps,
                                                                f16* y) {
     typedef f16 f16x8 __attribute__((ext_vector_type(8)));

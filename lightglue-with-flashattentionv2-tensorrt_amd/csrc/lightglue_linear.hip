@@ -1345,8 +1345,8 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
         return bad("lg_linear_cat_ln_gelu");
     if (m == 0) return MHA_HD64_STATUS_SUCCESS;
     const int lnf = g_ln_fused.load();  // 1: by size; 2: at every size (A/B)
-    const bool big = (m + 127) / 128 >= kTileGrid;  // a full round of 128-row tiles
-    const bool fused = lnf && n == kLnN && (lnf == 2 || big || (m + 63) / 64 >= kTileGrid) && aligned16(bias) && aligned16(gamma) &&
+    const bool big = m >= 128 * kTileGrid;  // a full round of 128-row tiles (32,768 rows)
+    const bool fused = lnf && n == kLnN && (lnf == 2 || big || m >= 64 * kTileGrid) && aligned16(bias) && aligned16(gamma) &&
                        aligned16(beta) && aligned16(out) && wide_mode() != 0;
     if (!fused) {  // the projection, then LayerNorm+GELU in place (lightglue_glue.hip)
         const int32_t st = lg_linear_cat(x, ctx0, ctx1, heads, n0, n1, pairs, w, bias, n, out, stream);
@@ -1388,7 +1388,7 @@ int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int
         return bad("lg_linear_cat_ffn");
     if (m == 0) return MHA_HD64_STATUS_SUCCESS;
     const int lnf = g_ln_fused.load();  // as lg_linear_cat_ln_gelu: 1 by size, 2 at every size, 0 never
-    const bool big = (m + 127) / 128 >= kTileGrid;
+    const bool big = m >= 128 * kTileGrid;
     const bool fused = lnf && g_ffn_fused.load() && k == kLnN && d == kFfnOut && (lnf == 2 || big) && aligned16(b1) && aligned16(gamma) &&
                        aligned16(beta) && aligned16(b2) && aligned16(out) && wide_mode() != 0;
     if (!fused) {  // h in the caller's buffer, then the output projection with the residual

@@ -183,13 +183,24 @@ def load() -> ctypes.CDLL:
     except Exception:  # pragma: no cover
         pass
     lib = ctypes.CDLL(LIB_PATH)
+    stale = (f"{LIB_PATH} is stale (built from older sources than this package binds): rebuild it with "
+             f"`make -C {PKG_DIR}`")
+    # the version first: a library older than the query lacks it (and other symbols bound below)
+    try:
+        ver_fn = lib.lg_glue_abi_version
+    except AttributeError:
+        raise LibraryMissing(f"{stale}; it has no lg_glue_abi_version") from None
+    ver_fn.argtypes, ver_fn.restype = [], _I
+    if ver_fn() != GLUE_ABI_VERSION:  # the argument lists below match this ABI only
+        raise LibraryMissing(f"{stale}; glue ABI {ver_fn()}, this package binds {GLUE_ABI_VERSION}")
     for table in (SIGNATURES, HOOKS):
         for name, (args, res) in table.items():
-            fn = getattr(lib, name)
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                raise LibraryMissing(f"{stale}; it does not export {name}") from None
             fn.argtypes = args
             fn.restype = res
-    if lib.lg_glue_abi_version() != GLUE_ABI_VERSION:  # the argument lists below match ABI 2 only
-        raise LibraryMissing(f"{LIB_PATH}: glue ABI {lib.lg_glue_abi_version()}, this package binds {GLUE_ABI_VERSION}")
     _lib = lib
     return lib
 

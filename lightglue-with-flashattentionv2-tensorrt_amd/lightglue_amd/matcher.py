@@ -456,10 +456,12 @@ class MatchAssignment(nn.Module):
 
     def forward_rows(self, x: torch.Tensor, pr: int, m: int, n: int) -> torch.Tensor:
         """fp16 hip path on both images' rows x [1, P*(m+n), d] at once: ONE projection with
-        [W_final / scale ; w_match ; 0] (d^0.25 = 4 for d = 256: the scaling is exact in fp16, so
-        this equals fp16(final_proj(d)) / scale), the similarity as one batched GEMM on the fp16
-        halves, and the dual log-softmax reading the fp16 similarity and the matchability channel
-        directly (lightglue.py:208-233)."""
+        [W_final / scale ; w_match ; 0], the similarity as one batched GEMM on the fp16 halves, and
+        the dual log-softmax reading the fp16 similarity and the matchability channel directly
+        (lightglue.py:208-233). d^0.25 = 4 for d = 256, a power of two: dividing W and b by it is
+        exact unless a quotient falls below 2^-14 (fp16 subnormals), where it loses up to 2 bits; so
+        the output equals the reference's fp16(final_proj(d)) / scale except for weights, biases or
+        outputs that small, which differ by at most that subnormal rounding."""
         d = x.shape[-1]
         fp, mt = self.final_proj, self.matchability
 
@@ -523,6 +525,15 @@ class LightGlueMatcher(nn.Module):
             raise ValueError("glue must be 'hip' or 'torch'")
         self.glue = glue
 
+    def pair_inputs_ok(self, kpts0, kpts1, desc0, desc1) -> bool:
+        """lg_pair_inputs reads both descriptor sets, both keypoint sets and posenc.Wr as raw fp16
+        [.., 256] / [.., 2] / [32, 2] rows: take it only when every one of them is exactly that (an
+        fp32 model or mixed-dtype inputs take the framework path, which casts or raises)."""
+        f16 = torch.float16
+        return (isinstance(self.input_proj, nn.Identity) and all(t.dtype == f16 for t in (kpts0, kpts1, desc0, desc1))
+                and self.posenc.Wr.weight.dtype == f16 and desc0.shape[-1] == 256 and desc1.shape[-1] == 256
+                and kpts0.shape[-1] == 2 and kpts1.shape[-1] == 2 and tuple(self.posenc.Wr.weight.shape) == (32, 2))
+
     def forward(self, kpts0, kpts1, desc0, desc1):
         pr, m, n = desc0.shape[0], desc0.shape[1], desc1.shape[1]
         hip = self.glue == "hip"
@@ -533,9 +544,7 @@ class LightGlueMatcher(nn.Module):
         rows = pr * (m + n)
         if hip and not desc0.is_cuda:
             raise PluginError("LightGlueMatcher(glue='hip') runs on the GPU only (no CPU fallback)")
-        fast = hip and desc0.dtype == torch.float16 and isinstance(self.input_proj, nn.Identity) and \
-            desc0.shape[-1] == 256 and kpts0.dtype == torch.float16
-        if fast:  # pair-major rows and the positional encoding in one launch
+        if hip and self.pair_inputs_ok(kpts0, kpts1, desc0, desc1):  # pair-major rows + posenc in one launch
             x, cos, sin = _Hip.pair_inputs(desc0, desc1, kpts0, kpts1, self.posenc.Wr.weight)
         else:
             x = self.input_proj(torch.cat((desc0, desc1), 1))          # [P, M+N, d], pair-major rows

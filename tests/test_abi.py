@@ -4,6 +4,7 @@ include/mha_hd64.h declares, and the plugin's host-side contract mirrors the ref
 import ctypes
 import os
 import re
+import shutil
 import subprocess
 import sys
 
@@ -436,3 +437,24 @@ def test_ffn_and_form_hooks_validate_before_touching_the_device(lib):
         assert lib.lg_linear_set_ffn_fused(0) == 1
     finally:
         lib.lg_linear_set_ffn_fused(prev)
+
+
+@pytest.mark.parametrize("version", [None, 1])
+def test_stale_library_is_reported_as_missing(tmp_path, monkeypatch, version):
+    """A library built from older sources (no lg_glue_abi_version, or an older ABI) raises
+    LibraryMissing naming the rebuild, not an AttributeError from the binding loop."""
+    if not shutil.which("gcc"):
+        pytest.skip("needs gcc")
+    from lightglue_amd import _lib
+
+    src = tmp_path / "stale.c"
+    body = "int mha_hd64_get_nb_outputs(void) { return 1; }\n"
+    if version is not None:
+        body += f"int lg_glue_abi_version(void) {{ return {version}; }}\n"
+    src.write_text(body)
+    so = tmp_path / "libstale.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", str(src), "-o", str(so)], check=True)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(so))
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.raises(_lib.LibraryMissing, match="stale"):
+        _lib.load()

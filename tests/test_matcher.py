@@ -104,6 +104,23 @@ def test_default_attention_refuses_cpu(glue):
             model(*pair)
 
 
+def test_pair_inputs_fast_path_needs_every_operand_fp16():
+    """lg_pair_inputs reads desc0/desc1/kpts0/kpts1/posenc.Wr as raw fp16: the fast path is taken only
+    when all five are fp16 (and 256 / 2 wide); any fp32 operand takes the framework path."""
+    from lightglue_amd import matcher
+
+    m = matcher.LightGlueMatcher(n_layers=1, attention=_oracle_attention).eval()
+    k0, k1, d0, d1 = (t.half() for t in matcher.synthetic_pair(3, 16, 12))
+    assert not m.pair_inputs_ok(k0, k1, d0, d1)            # fp32 model: Wr is fp32
+    m = m.half()
+    assert m.pair_inputs_ok(k0, k1, d0, d1)
+    for i in range(4):
+        args = [k0, k1, d0, d1]
+        args[i] = args[i].float()
+        assert not m.pair_inputs_ok(*args), i
+    assert not m.pair_inputs_ok(k0, k1, d0, d1[..., :128])
+
+
 def _gpu_run(name, dtype, glue="hip"):
     model, _, pair = _model(name, glue=glue)
     dev = torch.device("cuda:0")
