@@ -17,6 +17,8 @@
  * and `batch` in the dual log-softmax and its workspace query. A host built against an older
  * header links against the same symbol names and would pass shifted arguments: check
  * lg_glue_abi_version() == LG_GLUE_ABI_VERSION once at load.
+ * ABI version 3 (round 6): lg_linear_cat_ffn takes the packed weight stream of its one-launch form
+ * (w_packed, after b2; lg_ffn_pack).
  */
 #ifndef LIGHTGLUE_GLUE_H_
 #define LIGHTGLUE_GLUE_H_
@@ -30,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LG_GLUE_ABI_VERSION 2
+#define LG_GLUE_ABI_VERSION 3
 /* The ABI version of the argument lists below that this library implements. */
 int32_t lg_glue_abi_version(void);
 
@@ -90,14 +92,26 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
                               float eps, void* out, hipStream_t stream);
 /* lg_linear_cat_ffn:    the whole FFN with the block's residual (lightglue.py:101-106, 150-151 / 174-175):
  *                       out [n0+n1, d] = x + fp16(W2 · GELU(LayerNorm(W1 · [x | merge_heads(ctx0, ctx1)] + b1)) + b2)
- *                       with d = heads*64 = 256, W1 [2d, 2d], W2 [d, 2d]: lg_linear_cat_ln_gelu into h [m, 2d]
- *                       then lg_linear(h, W2, b2, res = x); with lg_linear_set_ffn_fused(1), one launch
- *                       (ffn_kernel: the GELU output stays in LDS) where lg_linear_cat_ln_gelu takes its
- *                       128-row one-launch form (m >= 32,768, or lg_linear_set_ln_fused(2)), bitwise equal.
- *                       h must hold m*2d fp16 either way; out must not alias x (16-B aligned pointers). */
+ *                       with d = heads*64 = 256, W1 [2d, 2d], W2 [d, 2d]. With w_packed (W1 and W2 as
+ *                       lg_ffn_pack lays them out) and up to 8,192 rows (one to four image pairs of 1,024
+ *                       keypoints): ONE launch, 32 rows per workgroup (ffn_rows_kernel: each wave streams
+ *                       its own weight fragments into registers, the GELU output stays in LDS; within 2
+ *                       fp16 ulps of the two calls). Otherwise (w_packed NULL, or more rows):
+ *                       lg_linear_cat_ln_gelu into h [m, 2d] then lg_linear(h, W2, b2, res = x); see
+ *                       lg_linear_set_ffn_fused. h must hold m*2d fp16 either way; out must not alias x
+ *                       (16-B aligned pointers). */
 int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
                           int32_t pairs, const void* w1, const void* b1, const void* gamma, const void* beta, float eps,
-                          const void* w2, const void* b2, void* h, void* out, hipStream_t stream);
+                          const void* w2, const void* b2, const void* w_packed, void* h, void* out, hipStream_t stream);
+/* lg_ffn_pack:          W1 [2d, 2d] and W2 [d, 2d] (nn.Linear layout, fp16, d = heads*64 = 256) re-laid as
+ *                       the one-launch FFN reads them: 8 wave streams of 96 KiB, stream w = 64 KiB of W1
+ *                       rows 64w..64w+63 then 32 KiB of W2 rows 32w..32w+31, in 1-KiB pieces i (W1: step j,
+ *                       block b at i = 2j + b; W2: step j at i = 64 + j) whose 16-B lane l holds
+ *                       W[row0 + 32b + (l % 32)][16j + 8(l / 32) .. + 8] — every load of the kernel one
+ *                       contiguous KiB. lg_ffn_packed_bytes(heads): its size (786,432 B; 0 if heads != 4).
+ *                       Weights are static: pack once per weight update. */
+size_t lg_ffn_packed_bytes(int32_t heads);
+int32_t lg_ffn_pack(const void* w1, const void* w2, int32_t heads, void* packed, hipStream_t stream);
 /* lg_linear_qkv_rotary: SelfBlock projection (lightglue.py:111-134) with W's rows and the bias in
  *                       [q|k|v][head][dim] order (row j*heads*64 + h*64 + d = Wqkv row (h*64+d)*3 + j):
  *                       rotary (cos/sin [n0+n1, 64]) on q and k in fp16 arithmetic, as the reference's
@@ -152,10 +166,12 @@ int32_t lg_linear_set_wide(int32_t mode);
  * round of its tiles on, 0 always two launches, 2 always one launch (A/B). The forms agree within fp16
  * rounding, not in every bit (the one-launch variance is two-pass). Returns the previous setting. */
 int32_t lg_linear_set_ln_fused(int32_t on);
-/* Test and benchmark hook for lg_linear_cat_ffn: 0 (the default) its two calls, 1 its one launch
- * wherever lg_linear_cat_ln_gelu takes its 128-row one-launch form (measured slower: an A/B path).
- * Returns the previous value. */
-int32_t lg_linear_set_ffn_fused(int32_t on);
+/* Test and benchmark hook for lg_linear_cat_ffn's forms: 1 (the default) by size — the one-launch
+ * 32-row form up to 8,192 rows when w_packed is given, the two calls otherwise; 0 always the two
+ * calls; 2 the 32-row form at every size (w_packed given); 3 the 128-row one-launch form (ffn_kernel,
+ * bitwise equal to the two calls) where lg_linear_cat_ln_gelu takes its 128-row form (A/B). Values
+ * outside 0..3 are clamped. Returns the previous mode. */
+int32_t lg_linear_set_ffn_fused(int32_t mode);
 
 #ifdef __cplusplus
 }

@@ -1177,6 +1177,226 @@ __global__ __launch_bounds__(512, 1) void ffn_kernel(LinArgs p, const f16* __res
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---- the whole FFN for launches of few rows (lg_linear_cat_ffn at P = 1..4 pairs, round 6) ----
+// out = x + fp16(W2 · GELU(LN(fp16(W1 · [x | heads] + b1))) + b2) with one workgroup per 32 rows: at
+// a single image pair (M = 1,024..4,096) the FFN was three launches of ~5 us each, every one of them
+// near the launch floor (profiles/r05/single_pair_timelines.txt: 269 of 557 us of a forward at n =
+// 1,024). Here one launch: 8 waves, wave w owns hidden channels [64w, 64w + 64) in phase 1 and output
+// channels [32w, 32w + 32) in phase 2, so every weight fragment a wave multiplies is its own — W1 and
+// W2 stream from L2 straight into VGPRs in the MFMA A-operand layout (lane (r, hh): row r of the
+// wave's 32-channel block, k = 16 s + 8 hh .. + 8 of step s; lg_ffn_pack stores them in that order),
+// D steps ahead, as ONE stream that runs from phase 1 into phase 2 (W2's first fragments load under
+// the LayerNorm); no barrier in either GEMM loop. The 32 activation rows [x | heads] (the A-gather of lg_linear_cat) sit in LDS for the
+// whole launch (32 KiB, rows of 1 KiB with 16-B units XOR (row & 15): conflict-free ds_read_b128 of
+// 16 rows at one k), as does GELU's output h (the second GEMM's B operand, the same layout), and the
+// residual x is read back from the A tile. Per workgroup the weights are 768 KiB, the bound of this
+// form (~12 k cycles at the ~64 B/clk a CU takes in), whatever the rows per workgroup: 32 rows keep
+// the MFMA work (6 k cycles per SIMD) under it with the fewest workgroups re-reading W.
+// Arithmetic: h = fp16(acc + b1) and the output fp16(fp16(acc + b2) + x) as lin_val / res_add (the
+// k16 blocks in the 64 x 64 form's order: h before the LayerNorm and the second product given h are
+// bitwise those of the two-call path); LayerNorm two-pass over the row's 512 values (mean, then the
+// sum of squared deviations; fixed reduction order), normalisation and GELU as linear_ln_kernel.
+constexpr int kFrMT = 32;             // rows per workgroup
+constexpr int kFrMaxRows = 256 * kFrMT;  // the by-size choice: one round of workgroups (8,192 rows)
+constexpr int kFfnPackedBytes = (512 * 512 + 256 * 512) * 2;  // lg_ffn_pack: 8 wave streams of 96 KiB
+template <int D>
+__global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* __restrict__ gamma,
+                                                          const f16* __restrict__ beta, float eps,
+                                                          const f16* __restrict__ wp, const f16* __restrict__ b2) {
+    constexpr int K = 512, NO = kFfnOut;           // FFN width (= hidden), output channels
+    constexpr int kA = 0, kH = kFrMT * K * 2;      // A and h tiles, [32][1 KiB] each
+    constexpr int kStg = 2 * kH;                   // output staging, 2.5 KiB per wave ([32][80 B])
+    constexpr int kPar = kStg + 8 * kFrMT * 80;    // b1, gamma, beta [512], b2 [256] fp16
+    constexpr int kRed = kPar + (3 * K + NO) * 2;  // row partials [2][32][8 waves] fp32
+    constexpr int NS1 = K / 16, NS = 2 * NS1;      // k16 steps per GEMM; the stream: phase 1, then 2
+    static_assert(D >= 1 && D <= NS1, "prefetch depth");
+    __shared__ __attribute__((aligned(16))) char smem[kRed + 2 * kFrMT * 8 * 4];
+    lds_char* const lds = (lds_char*)smem;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, hh = lane >> 5;
+    const int m0 = blockIdx.x * kFrMT;
+
+    // ---- A tile: row 8 i + wave, 16-B unit `lane` (x: units 0..31, head h of the attention output:
+    // units 32 + 8 h .. + 7), loaded whole-row coalesced; rows past m repeat row m - 1 ----
+    f16x8 av[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int grow = min(m0 + 8 * i + wave, p.m - 1);
+        const f16* src;
+        if (lane < 32) {
+            src = p.a + (size_t)grow * (K / 2) + lane * 8;
+        } else {
+            const LinRow lr = lin_row(p, grow, (lane - 32) >> 3);
+            src = (lr.first ? p.ctx0 : p.ctx1) + lr.off + ((lane - 32) & 7) * 8;
+        }
+        av[i] = *reinterpret_cast<const f16x8*>(src);
+    }
+    // the epilogue vectors: b1 / gamma / beta (64 units each) and b2 (32 units)
+    f16x8 pv = {};
+    if (tid < 224) {
+        const f16* const pvs = tid < 64 ? p.bias : tid < 128 ? gamma : tid < 192 ? beta : b2;
+        pv = *reinterpret_cast<const f16x8*>(pvs + (tid & 63) * 8);
+    }
+
+    // ---- the weight stream (lg_ffn_pack's layout): wave w's 96 KiB, piece i at w * 96 KiB + i KiB,
+    // lane l's 16 B at + 16 l: step j of phase 1, block b = piece 2 j + b; step j of phase 2 = 64 + j.
+    // Every load is one contiguous KiB (whole 128-B lines: the row-major W's 32-B row pieces per
+    // lane fetched each line four times, 26 vs 12 us per launch at 2,048 rows) ----
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(wp), (short)0, kFfnPackedBytes, 0x00020000);
+    const unsigned wo = (unsigned)(wave * (kFfnPackedBytes / 8) + lane * 16);
+    auto wfrag = [&](int j, int b) {
+        const int i = j < NS1 ? 2 * j + b : NS1 + j;
+        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, wo, i * 1024, 0));
+    };
+    f16x8 q[D][2];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {  // (in stream order: the loop's counted waits assume it)
+        q[j][0] = wfrag(j, 0);
+        q[j][1] = wfrag(j, 1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // A and the vectors into LDS (the compiler's wait counts the weight loads issued after them)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = 8 * i + wave;
+        *(lds_f16x8*)(lds + kA + row * 1024 + ((lane ^ (row & 15)) << 4)) = av[i];
+    }
+    if (tid < 224) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    // B-operand fragment of step s from a [32][1 KiB] tile: row r, unit 2 s + hh
+    auto bfrag = [&](int base, int s) {
+        return *(lds_f16x8*)(lds + base + r * 1024 + (((2 * s + hh) ^ (r & 15)) << 4));
+    };
+    // ---- phase 1: hᵀ (the wave's 64 channels x 32 rows) = W1 · Aᵀ ----
+    // (each step's B fragment is read one step ahead: its LDS latency under the previous MFMAs)
+    f32x16 acc[2] = {};
+    f16x8 af = bfrag(kA, 0);
+#pragma unroll
+    for (int j = 0; j < NS1; ++j) {
+        const f16x8 wa = q[j % D][0], wb = q[j % D][1];
+        if (j + D < NS) {
+            q[j % D][0] = wfrag(j + D, 0);
+            if (j + D < NS1) q[j % D][1] = wfrag(j + D, 1);
+        }
+        const f16x8 an = j + 1 < NS1 ? bfrag(kA, j + 1) : af;
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa, af, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wb, af, acc[1], 0, 0, 0);
+        af = an;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- LayerNorm over the row's 512 h values: the wave's 64 are in lanes r and r + 32 ----
+    // lane (r, hh): acc[b][4 g + t] = hidden channel 64 w + 32 b + 8 g + 4 hh + t of row m0 + r
+    float* const red = (float*)(void*)(smem + kRed);  // [pass][row][wave]
+    float s = 0.f;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + (64 * wave + 32 * b + 8 * g + 4 * hh) * 2);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float h = (float)lin_val(acc[b][4 * g + t], b4[t]);
+                acc[b][4 * g + t] = h;
+                s += h;
+            }
+        }
+    s += __shfl_xor(s, 32, 64);
+    if (hh == 0) red[r * 8 + wave] = s;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    auto row_sum = [&](int off) {  // the 8 waves' partials of row r, in a fixed order
+        const f32x4 a = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (off + r * 8) * 4);
+        const f32x4 c = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (off + r * 8 + 4) * 4);
+        return ((a[0] + a[1]) + (a[2] + a[3])) + ((c[0] + c[1]) + (c[2] + c[3]));
+    };
+    const float mean = row_sum(0) * (1.f / K);
+    float qv = 0.f;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const float d = acc[b][e] - mean;
+            acc[b][e] = d;
+            qv = __builtin_fmaf(d, d, qv);
+        }
+    qv += __shfl_xor(qv, 32, 64);
+    if (hh == 0) red[kFrMT * 8 + r * 8 + wave] = qv;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const float rstd = __builtin_amdgcn_rsqf(row_sum(kFrMT * 8) * (1.f / K) + eps);
+    // GELU(LN(h)) -> fp16 into the h tile (unit 8 w + 4 b + g of row r, half hh)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = 64 * wave + 32 * b + 8 * g + 4 * hh;
+            const u32x2 g4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + K * 2 + n * 2);
+            const u32x2 be4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + 2 * K * 2 + n * 2);
+            f16x4 o;
+#pragma unroll
+            for (int u = 0; u < 4; u += 2) {
+                const f32x2 xr = f32x2{acc[b][4 * g + u], acc[b][4 * g + u + 1]} * rstd;
+                const f32x2 gl = gelu_as2(f32x2{mixf<0>(xr[0], g4[u >> 1], be4[u >> 1]), mixf<1>(xr[1], g4[u >> 1], be4[u >> 1])});
+                o[u] = (f16)gl[0];
+                o[u + 1] = (f16)gl[1];
+            }
+            *(__attribute__((address_space(3))) f16x4*)(lds + kH + r * 1024 + (((8 * wave + 4 * b + g) ^ (r & 15)) << 4) + 8 * hh) = o;
+        }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // h complete
+
+    // ---- phase 2: outᵀ (the wave's 32 channels x 32 rows) = W2 · hᵀ ----
+    f32x16 o2 = {};
+    f16x8 hf = bfrag(kH, 0);
+#pragma unroll
+    for (int j = NS1; j < NS; ++j) {
+        const f16x8 wa = q[j % D][0];
+        if (j + D < NS) q[j % D][0] = wfrag(j + D, 0);
+        const f16x8 hn = j + 1 < NS ? bfrag(kH, j + 1 - NS1) : hf;
+        o2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa, hf, o2, 0, 0, 0);
+        hf = hn;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- out = fp16(fp16(acc + b2) + x): the wave's 32 x 32 block staged row-major in its own LDS
+    // rows (80-B pitch), then two lanes a row, 32 B each, with x from the A tile ----
+    lds_char* const stg = lds + kStg + wave * (kFrMT * 80);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int c = 32 * wave + 8 * g + 4 * hh;
+        const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + 3 * K * 2 + c * 2);
+        const f16x4 v = f16x4{lin_val(o2[4 * g], b4[0]), lin_val(o2[4 * g + 1], b4[1]), lin_val(o2[4 * g + 2], b4[2]),
+                              lin_val(o2[4 * g + 3], b4[3])};
+        *(__attribute__((address_space(3))) f16x4*)(stg + r * 80 + (8 * g + 4 * hh) * 2) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the wave's own rows: LDS ops of a wave in order)
+    const int rr = lane >> 1, half = lane & 1;
+    if (m0 + rr < p.m) {
+#pragma unroll
+        for (int e2 = 0; e2 < 2; ++e2) {
+            f16x8 v = *(lds_f16x8*)(stg + rr * 80 + half * 32 + e2 * 16);
+            const f16x8 xr = *(lds_f16x8*)(lds + kA + rr * 1024 + (((4 * wave + 2 * half + e2) ^ (rr & 15)) << 4));
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], xr[e]);
+            *reinterpret_cast<f16x8*>(p.out[0] + (size_t)(m0 + rr) * NO + 32 * wave + 16 * half + 8 * e2) = v;
+        }
+    }
+}
+
+// lg_ffn_pack: one thread per 16-B fragment of the packed stream (layout: include/lightglue_glue.h)
+__global__ __launch_bounds__(256) void ffn_pack_kernel(const f16* __restrict__ w1, const f16* __restrict__ w2, f16* packed) {
+    const int f = blockIdx.x * 256 + threadIdx.x;  // fragment: wave w = f / 6144, piece i, lane l
+    if (f >= kFfnPackedBytes / 16) return;
+    const int w = f / 6144, i = (f % 6144) / 64, l = f % 64, r = l % 32, hh = l / 32;
+    const f16* src = i < 64 ? w1 + (size_t)(64 * w + 32 * (i & 1) + r) * 512 + 16 * (i >> 1) + 8 * hh
+                            : w2 + (size_t)(32 * w + r) * 512 + 16 * (i - 64) + 8 * hh;
+    *reinterpret_cast<f16x8*>(packed + (size_t)f * 8) = *reinterpret_cast<const f16x8*>(src);
+}
+
 constexpr int kTileGrid = 256;  // the 256-row forms: one workgroup per CU
 // lg_linear_cat_ln_gelu's one-launch form (linear_ln_kernel), by size: its 128-row tiles from one
 // full round of them on (256: M >= 32,768 rows, P >= 16 pairs of 1024 keypoints), its 64-row tiles
@@ -1195,7 +1415,12 @@ std::atomic<int> g_ln_fused{1};
 // per 128-row tile (4x the W bytes per row of lg_linear's 256 x 128 tiles: 7.5 us of L2 -> CU traffic),
 // and its epilogue (residual loads, the 16.8 MB store burst, 7.6 us) overlaps nothing with one tile per
 // workgroup, which costs more than h's HBM round trip saves. Kept as an A/B path (lg_linear_set_ffn_fused).
-std::atomic<int> g_ffn_fused{0};
+std::atomic<int> g_ffn_fused{1};
+// ffn_rows_kernel's weight-stream depth: k16 steps of fragments in flight per wave (A/B: -DLG_FR_DEPTH)
+#ifndef LG_FR_DEPTH
+#define LG_FR_DEPTH 12
+#endif
+constexpr int kFrDepth = LG_FR_DEPTH;
 // The tile form (tile_form below): lg_linear_set_wide(0..3) or LG_LINEAR_WIDE forces one (where n
 // allows), for tests and A/B timing; -1 (the default) chooses by size.
 std::atomic<int> g_wide{-2};
@@ -1380,17 +1605,31 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
 
 int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
                           int32_t pairs, const void* w1, const void* b1, const void* gamma, const void* beta, float eps,
-                          const void* w2, const void* b2, void* h, void* out, hipStream_t stream) {
+                          const void* w2, const void* b2, const void* w_packed, void* h, void* out, hipStream_t stream) {
     const int d = heads * kD, k = 2 * d, m = pairs * (n0 + n1);
     if (heads <= 0 || n0 < 0 || n1 < 0 || pairs < 0 || !shape_ok(m, k, k) || !x || !w1 || !b1 || !gamma || !beta || !w2 ||
         !b2 || !h || !out || out == x || !aligned16(x) || (n0 && !aligned16(ctx0)) || (n1 && !aligned16(ctx1)) ||
-        !aligned16(w1) || !aligned16(w2) || !aligned8(b1) || !aligned8(b2) || !aligned16(h) || !aligned8(out) || !(eps >= 0.f))
+        !aligned16(w1) || !aligned16(w2) || !aligned8(b1) || !aligned8(b2) || !aligned16(h) || !aligned8(out) || !(eps >= 0.f) ||
+        (w_packed && !aligned16(w_packed)))
         return bad("lg_linear_cat_ffn");
     if (m == 0) return MHA_HD64_STATUS_SUCCESS;
+    const int ffm = g_ffn_fused.load();  // 1 by size (default), 0 two calls, 2 ffn_rows_kernel always, 3 ffn_kernel (A/B)
+    const bool al = k == kLnN && d == kFfnOut && aligned16(b1) && aligned16(gamma) && aligned16(beta) && aligned16(b2) &&
+                    aligned16(out);
+    if (al && w_packed && ((ffm == 1 && m <= kFrMaxRows) || ffm == 2)) {  // few rows: the whole FFN, 32 rows a workgroup
+        LinArgs p{};
+        p.a = (const f16*)x, p.ctx0 = (const f16*)ctx0, p.ctx1 = (const f16*)ctx1, p.w = (const f16*)w1;
+        p.bias = (const f16*)b1, p.out[0] = (f16*)out;
+        p.m = m, p.n = k, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
+        hipLaunchKernelGGL((ffn_rows_kernel<kFrDepth>), dim3((m + kFrMT - 1) / kFrMT), dim3(512), 0, stream, p,
+                           (const f16*)gamma, (const f16*)beta, eps, (const f16*)w_packed, (const f16*)b2);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
+                               : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_linear_cat_ffn", hipGetErrorString(e));
+    }
     const int lnf = g_ln_fused.load();  // as lg_linear_cat_ln_gelu: 1 by size, 2 at every size, 0 never
     const bool big = m >= 128 * kTileGrid;
-    const bool fused = lnf && g_ffn_fused.load() && k == kLnN && d == kFfnOut && (lnf == 2 || big) && aligned16(b1) && aligned16(gamma) &&
-                       aligned16(beta) && aligned16(b2) && aligned16(out) && wide_mode() != 0;
+    const bool fused = lnf && ffm == 3 && al && (lnf == 2 || big) && wide_mode() != 0;
     if (!fused) {  // h in the caller's buffer, then the output projection with the residual
         const int32_t st = lg_linear_cat_ln_gelu(x, ctx0, ctx1, heads, n0, n1, pairs, w1, b1, gamma, beta, eps, h, stream);
         if (st != MHA_HD64_STATUS_SUCCESS) return st;
@@ -1408,6 +1647,17 @@ int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_linear_cat_ffn", hipGetErrorString(e));
+}
+
+size_t lg_ffn_packed_bytes(int32_t heads) { return heads == 4 ? (size_t)kFfnPackedBytes : 0; }
+
+int32_t lg_ffn_pack(const void* w1, const void* w2, int32_t heads, void* packed, hipStream_t stream) {
+    if (heads != 4 || !w1 || !w2 || !packed || !aligned16(w1) || !aligned16(w2) || !aligned16(packed)) return bad("lg_ffn_pack");
+    hipLaunchKernelGGL(ffn_pack_kernel, dim3(kFfnPackedBytes / 16 / 256), dim3(256), 0, stream, (const f16*)w1, (const f16*)w2,
+                       (f16*)packed);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
+                           : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_ffn_pack", hipGetErrorString(e));
 }
 
 int32_t lg_linear_qkv_rotary(const void* x, const void* w_perm, const void* b_perm, const void* cosv,
@@ -1455,6 +1705,6 @@ int32_t lg_diag_ln_stamps(void* host_dst) {  // (diagnostic build only: not in t
 }
 #endif
 int32_t lg_linear_set_ln_fused(int32_t on) { return g_ln_fused.exchange(on == 2 ? 2 : on ? 1 : 0); }
-int32_t lg_linear_set_ffn_fused(int32_t on) { return g_ffn_fused.exchange(on ? 1 : 0); }
+int32_t lg_linear_set_ffn_fused(int32_t mode) { return g_ffn_fused.exchange(mode < 0 ? 0 : (mode > 3 ? 3 : mode)); }
 
 }  // extern "C"

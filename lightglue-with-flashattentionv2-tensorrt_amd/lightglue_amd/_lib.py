@@ -133,7 +133,9 @@ SIGNATURES.update({
     "lg_linear": ([_P, _P, _P, _P, _I, _I, _I, _P, _P], _I),
     "lg_linear_cat": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P, _P], _I),
     "lg_linear_cat_ln_gelu": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, ctypes.c_float, _P, _P], _I),
-    "lg_linear_cat_ffn": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, ctypes.c_float, _P, _P, _P, _P, _P], _I),
+    "lg_linear_cat_ffn": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, ctypes.c_float, _P, _P, _P, _P, _P, _P], _I),
+    "lg_ffn_packed_bytes": ([_I], _S),
+    "lg_ffn_pack": ([_P, _P, _I, _P, _P], _I),
     "lg_linear_qkv_rotary": ([_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P], _I),
     "lg_linear_split2": ([_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P], _I),
     "lg_layernorm_gelu": ([_I, _P, _P, _P, _I, _I, ctypes.c_float, _P, _P], _I),
@@ -165,7 +167,7 @@ class LibraryMissing(RuntimeError):
     pass
 
 
-GLUE_ABI_VERSION = 2  # include/lightglue_glue.h LG_GLUE_ABI_VERSION
+GLUE_ABI_VERSION = 3  # include/lightglue_glue.h LG_GLUE_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

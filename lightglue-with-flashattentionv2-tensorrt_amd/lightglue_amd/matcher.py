@@ -122,18 +122,20 @@ class _Hip:
         return out
 
     @staticmethod
-    def ffn(x, c0, c1, w, b, ln: nn.LayerNorm, w2, b2):
+    def ffn(x, c0, c1, w, b, ln: nn.LayerNorm, w2, b2, packed=None):
         """x + ffn([x | merge_heads(c0, c1)]) (lightglue.py:101-106 with the block's residual):
-        linear_cat_ln_gelu into a scratch h, then linear(h, w2, b2, res=x) — or, with
-        lg_linear_set_ffn_fused(1), one launch (bitwise the same; measured slower, an A/B path)."""
+        with `packed` (ffn_pack(w, w2)) one launch up to 8,192 rows (ffn_rows_kernel), else
+        linear_cat_ln_gelu into the scratch h, then linear(h, w2, b2, res=x) (include/lightglue_glue.h,
+        lg_linear_set_ffn_fused)."""
         pr, heads, n0, n1 = c0.shape[0], c0.shape[1], c0.shape[2], c1.shape[2]
         m = pr * (n0 + n1)
         h = torch.empty((1, m, w.shape[0]), dtype=x.dtype, device=x.device)
         out = torch.empty((1, m, w2.shape[0]), dtype=x.dtype, device=x.device)
         st = _lib.load().lg_linear_cat_ffn(x.data_ptr(), c0.data_ptr(), c1.data_ptr(), heads, n0, n1, pr,
                                            w.data_ptr(), b.data_ptr(), ln.weight.data_ptr(), ln.bias.data_ptr(),
-                                           float(ln.eps), w2.data_ptr(), b2.data_ptr(), h.data_ptr(), out.data_ptr(),
-                                           _Hip._stream(x))
+                                           float(ln.eps), w2.data_ptr(), b2.data_ptr(),
+                                           packed.data_ptr() if packed is not None else None, h.data_ptr(),
+                                           out.data_ptr(), _Hip._stream(x))
         _check(st, "lg_linear_cat_ffn")
         return out
 
@@ -258,6 +260,26 @@ def _ffn_in_fused(block: nn.Module, proj: nn.Linear, dtype: torch.dtype):
         return (torch.cat((wx, wm @ proj.weight.float()), 1), lin.bias.float() + wm @ proj.bias.float())
 
     return _cached(block, "_ffn_in_fused", (lin.weight, lin.bias, proj.weight, proj.bias), dtype, build)
+
+
+def ffn_pack(w1: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
+    """The one-launch FFN's weight stream (lg_ffn_pack, include/lightglue_glue.h) by tensor ops: for
+    wave w of 8, W1 rows 64w.. as pieces (step j, block b) then W2 rows 32w.. as pieces (step j), each
+    piece's 16-B lane l = W[row0 + 32b + l % 32][16j + 8(l // 32) : + 8]."""
+    p1 = w1.reshape(8, 2, 32, 32, 2, 8).permute(0, 3, 1, 4, 2, 5)   # (w, j, b, hh, r, e)
+    p2 = w2.reshape(8, 32, 32, 2, 8).permute(0, 2, 3, 1, 4)         # (w, j, hh, r, e)
+    return torch.cat((p1.reshape(8, -1), p2.reshape(8, -1)), 1).reshape(-1).contiguous()
+
+
+def _ffn_packed(block: nn.Module, proj: nn.Linear, dtype: torch.dtype):
+    """ffn_pack of the block's folded FFN input weight and its output weight (cached like them)."""
+    lin, out = block.ffn[0], block.ffn[3]
+
+    def build():
+        w, _ = _ffn_in_fused(block, proj, dtype)
+        return (ffn_pack(w, out.weight.to(dtype)),)
+
+    return _cached(block, "_ffn_packed", (lin.weight, lin.bias, proj.weight, proj.bias, out.weight), dtype, build)[0]
 
 
 def _qkv_perm(block: nn.Module, dtype: torch.dtype):
@@ -417,22 +439,23 @@ class TransformerLayer(nn.Module):
 
 
     def _forward_fused(self, x, cos, sin, splits, attention: AttnFn):
-        """fp16 hip path: 4 launches per block -- projection (+rotary/head split), grouped
-        attention, FFN input projection gathering [x | heads] (message projection folded in) with
-        LayerNorm+GELU in its epilogue, FFN output projection + residual (lg_linear_cat_ffn)."""
+        """fp16 hip path per block: projection (+rotary/head split), grouped attention, and the FFN
+        with its residual (lg_linear_cat_ffn: one launch up to 8,192 rows, else the input projection
+        gathering [x | heads] with LayerNorm+GELU, then the output projection + residual); the message
+        projection is folded into the FFN's first weight."""
         sa, ca = self.self_attn, self.cross_attn
         wq, bq = _qkv_perm(sa, x.dtype)
         qkv = _Hip.linear_qkv_rotary(x, wq, bq, cos, sin, sa.heads, splits)
         c0, c1 = attention(qkv)                                          # self0, self1: one launch
         w0, b0 = _ffn_in_fused(sa, sa.out_proj, x.dtype)
-        x = _Hip.ffn(x, c0, c1, w0, b0, sa.ffn[1], sa.ffn[3].weight, sa.ffn[3].bias)
+        x = _Hip.ffn(x, c0, c1, w0, b0, sa.ffn[1], sa.ffn[3].weight, sa.ffn[3].bias, _ffn_packed(sa, sa.out_proj, x.dtype))
         wc, bc = _cached(ca, "_qkv_stacked", (ca.to_qk.weight, ca.to_qk.bias, ca.to_v.weight, ca.to_v.bias),
                          x.dtype, lambda: (torch.cat((ca.to_qk.weight, ca.to_v.weight), 0),
                                            torch.cat((ca.to_qk.bias, ca.to_v.bias), 0)))
         (qk0, qk1), (v0, v1) = _Hip.linear_split2(x, wc, bc, ca.heads, splits)
         m0, m1 = attention([(qk0, qk1, v1), (qk1, qk0, v0)])            # cross: one launch
         w0, b0 = _ffn_in_fused(ca, ca.to_out, x.dtype)
-        return _Hip.ffn(x, m0, m1, w0, b0, ca.ffn[1], ca.ffn[3].weight, ca.ffn[3].bias)
+        return _Hip.ffn(x, m0, m1, w0, b0, ca.ffn[1], ca.ffn[3].weight, ca.ffn[3].bias, _ffn_packed(ca, ca.to_out, x.dtype))
 
 
 def log_double_softmax(sim: torch.Tensor, z0: torch.Tensor, z1: torch.Tensor) -> torch.Tensor:

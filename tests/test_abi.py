@@ -415,26 +415,31 @@ def test_ffn_and_form_hooks_validate_before_touching_the_device(lib):
     """lg_linear_cat_ffn (include/lightglue_glue.h) rejects bad arguments and returns success for an
     empty launch without a device call; the form hooks return the previous value and clamp."""
     A = 4096  # a fake 16-B aligned address: never dereferenced on these paths
-    args = dict(x=A, c0=A, c1=A, heads=4, n0=8, n1=8, pairs=1, w1=A, b1=A, g=A, be=A, eps=1e-5, w2=A, b2=A, h=A, out=2 * A)
+    args = dict(x=A, c0=A, c1=A, heads=4, n0=8, n1=8, pairs=1, w1=A, b1=A, g=A, be=A, eps=1e-5, w2=A, b2=A, wp=A, h=A,
+                out=2 * A)
 
     def call(**kw):
         a = {**args, **kw}
         return lib.lg_linear_cat_ffn(a["x"], a["c0"], a["c1"], a["heads"], a["n0"], a["n1"], a["pairs"], a["w1"], a["b1"],
-                                     a["g"], a["be"], a["eps"], a["w2"], a["b2"], a["h"], a["out"], None)
+                                     a["g"], a["be"], a["eps"], a["w2"], a["b2"], a["wp"], a["h"], a["out"], None)
 
-    assert call(pairs=0) == 0                     # nothing to launch
+    assert call(pairs=0) == 0 and call(pairs=0, wp=None) == 0  # nothing to launch
     for bad in (dict(x=None), dict(w2=None), dict(h=None), dict(out=A), dict(out=A + 4), dict(heads=0),
-                dict(heads=3), dict(pairs=-1), dict(eps=-1.0), dict(x=A + 8)):
+                dict(heads=3), dict(pairs=-1), dict(eps=-1.0), dict(x=A + 8), dict(wp=A + 8)):
         assert call(**{**bad, "pairs": 0 if "pairs" not in bad else bad["pairs"]}) == 1, bad
+    assert lib.lg_ffn_packed_bytes(4) == (512 * 512 + 256 * 512) * 2 and lib.lg_ffn_packed_bytes(3) == 0
+    for bad in ((A, A, 3, A), (None, A, 4, A), (A, A, 4, None), (A, A + 4, 4, A)):
+        assert lib.lg_ffn_pack(*bad, None) == 1, bad
     prev = lib.lg_linear_set_wide(7)              # clamped to 5
     try:
         assert lib.lg_linear_set_wide(-5) == 5    # clamped to -1
         assert lib.lg_linear_set_wide(4) == -1
     finally:
         lib.lg_linear_set_wide(prev)
-    prev = lib.lg_linear_set_ffn_fused(3)         # any nonzero: 1
+    prev = lib.lg_linear_set_ffn_fused(7)         # clamped to 3
     try:
-        assert lib.lg_linear_set_ffn_fused(0) == 1
+        assert lib.lg_linear_set_ffn_fused(-2) == 3   # clamped to 0
+        assert lib.lg_linear_set_ffn_fused(1) == 0
     finally:
         lib.lg_linear_set_ffn_fused(prev)
 

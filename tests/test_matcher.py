@@ -121,6 +121,24 @@ def test_pair_inputs_fast_path_needs_every_operand_fp16():
     assert not m.pair_inputs_ok(k0, k1, d0, d1[..., :128])
 
 
+def test_ffn_pack_layout():
+    """ffn_pack (the one-launch FFN's weight stream, include/lightglue_glue.h lg_ffn_pack): wave w's
+    96 KiB = W1 pieces i = 2j + b, then W2 pieces 64 + j; lane l of a piece = W[row0 + 32b + l % 32]
+    [16j + 8(l // 32) : + 8]. Every fragment checked against that definition."""
+    from lightglue_amd import matcher
+
+    w1 = torch.arange(512 * 512, dtype=torch.float32).reshape(512, 512)
+    w2 = -torch.arange(256 * 512, dtype=torch.float32).reshape(256, 512)
+    got = matcher.ffn_pack(w1, w2).reshape(8, 96, 64, 8)
+    w, i, l = torch.meshgrid(torch.arange(8), torch.arange(96), torch.arange(64), indexing="ij")
+    r, hh = l % 32, l // 32
+    e = torch.arange(8)
+    j1, b = (i // 2).clamp(max=31), i % 2
+    exp1 = w1[(64 * w + 32 * b + r)[..., None], (16 * j1 + 8 * hh)[..., None] + e]
+    exp2 = w2[(32 * w + r)[..., None].clamp(max=255), (16 * (i - 64).clamp(min=0) + 8 * hh)[..., None] + e]
+    assert torch.equal(got, torch.where((i < 64)[..., None], exp1, exp2))
+
+
 def _gpu_run(name, dtype, glue="hip"):
     model, _, pair = _model(name, glue=glue)
     dev = torch.device("cuda:0")
@@ -622,8 +640,9 @@ def test_linear_cat_ln_gelu_matches_torch(pairs, n0, n1):
 @pytest.mark.parametrize("pairs,n0,n1", [(16, 1024, 1024), (32, 1024, 1024), (17, 1000, 977), (1, 300, 257), (2, 64, 1)])
 def test_linear_cat_ffn_equals_two_calls(pairs, n0, n1):
     """lg_linear_cat_ffn (the whole FFN with the residual, lightglue.py:101-106 + :150-151) against
-    the two calls it makes by default: lg_linear_cat_ln_gelu then lg_linear(h, W2, b2, res = x). Its
-    one-launch form (lg_linear_set_ffn_fused(1): ffn_kernel, the GELU output kept in LDS, the second
+    its two calls (lg_linear_set_ffn_fused(0)): lg_linear_cat_ln_gelu then lg_linear(h, W2, b2, res = x),
+    the default above 8,192 rows (below it, ffn_rows_kernel: test_ffn_rows_kernel). Its 128-row
+    one-launch form (lg_linear_set_ffn_fused(3): ffn_kernel, the GELU output kept in LDS, the second
     GEMM's W2 fragments from global memory) runs the same operations in the same order, so the outputs
     are bitwise equal: at lg_linear_cat_ln_gelu's choice (one launch from 32,768 rows: P = 16 / 32;
     two calls below), the one-launch form forced at
@@ -649,9 +668,10 @@ def test_linear_cat_ffn_equals_two_calls(pairs, n0, n1):
         ln.bias.copy_(0.1 * rnd(512))
         outs = {}
         hh = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)
+        prev_f = lib.lg_linear_set_ffn_fused(0)
         default = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2)  # two calls (lg_linear_set_ffn_fused(0))
         two = mt._Hip.linear(hh, w2, b2, res=x)
-        prev_f = lib.lg_linear_set_ffn_fused(1)
+        lib.lg_linear_set_ffn_fused(3)
         try:
             for mode in (1, 2, 0):
                 prev = lib.lg_linear_set_ln_fused(mode)
@@ -676,6 +696,79 @@ def test_linear_cat_ffn_equals_two_calls(pairs, n0, n1):
             assert d <= 4e-3, (mode, d)
         else:
             assert torch.equal(outs[mode], outs[(mode, "two")]), (mode, d)
+
+
+def _ffn_torch(x, c0, c1, w, b, ln, w2, b2):
+    """The FFN with its residual as the fp16 model rounds it (lightglue.py:101-106, 150-151): F.linear
+    outputs rounded to fp16, LayerNorm and exact GELU in fp32 rounded to fp16, x + that in fp32 rounded."""
+    F = torch.nn.functional
+    a = torch.cat((x[0], torch.cat([torch.cat([ci[p].transpose(0, 1).reshape(ci.shape[2], -1) for ci in (c0, c1)], 0)
+                                     for p in range(c0.shape[0])], 0)), 1).float()
+    h = (a @ w.float().t() + b.float()).half().float()
+    g = F.gelu(F.layer_norm(h, (512,), ln.weight.float(), ln.bias.float(), ln.eps)).half().float()
+    o = (g @ w2.float().t() + b2.float()).half().float()
+    return (x[0].float() + o).half()[None]
+
+
+# |ffn_rows_kernel - two calls|: h before the LayerNorm is bitwise the two-call path's; the statistics
+# are two-pass where lg_layernorm_gelu takes E[h^2] - mean^2, so a GELU output can move by one fp16 ulp,
+# and with it the rounding of v = fp16(W2 g + b2) and of x + v. Bound: 2 ulp of the larger of |out|
+# and |v| = |out - x| (and 2^-11 near 0).
+def _ulp_bound(out, x, k=2.0):
+    mag = torch.maximum(out.float().abs(), (out.float() - x.float()).abs())
+    return k * torch.clamp(mag, min=2.0 ** -2) * 2.0 ** -10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pairs,n0,n1", [(1, 512, 512), (1, 1024, 1024), (1, 2048, 2048), (1, 700, 1301), (1, 1, 63),
+                                         (3, 37, 70), (4, 1024, 1024), (5, 1000, 1011), (1, 3, 2)])
+def test_ffn_rows_kernel(pairs, n0, n1):
+    """lg_linear_cat_ffn's one-launch form for few rows (ffn_rows_kernel, 32 rows per workgroup, the
+    default up to 8,192 rows; lg_linear_set_ffn_fused(2) forces it) against its two calls (0) and the
+    torch restatement of the fp16 model (_ffn_torch): single pairs of 512 / 1024 / 2048 keypoints,
+    ragged rows (a partial last workgroup, images of 1..3 rows), 4 pairs (8,192 rows: the last size the
+    default takes it) and 5 pairs forced (past it)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lightglue_amd import _lib
+    from lightglue_amd import matcher as mt
+
+    dev, dt, h = torch.device("cuda:0"), torch.float16, 4
+    lib = _lib.load()
+    gen = torch.Generator().manual_seed(21 + pairs + n0)
+    rnd = lambda *s: torch.randn(*s, generator=gen).to(dev, dt)  # noqa: E731
+    m = pairs * (n0 + n1)
+    with torch.no_grad():
+        x = rnd(1, m, 256) * 0.5
+        c0, c1 = rnd(pairs, h, n0, 64), rnd(pairs, h, n1, 64)
+        w, b = rnd(512, 512) * 0.05, rnd(512) * 0.1
+        w2, b2 = rnd(256, 512) * 0.05, rnd(256) * 0.1
+        ln = torch.nn.LayerNorm(512).to(dev, dt)
+        ln.weight.copy_(1 + 0.1 * rnd(512))
+        ln.bias.copy_(0.1 * rnd(512))
+        wp = mt.ffn_pack(w, w2)
+        packed_c = torch.empty(lib.lg_ffn_packed_bytes(h) // 2, dtype=dt, device=dev)
+        assert lib.lg_ffn_pack(w.data_ptr(), w2.data_ptr(), h, packed_c.data_ptr(), None) == 0
+        outs = {}
+        for mode in (0, 2, 1):
+            prev = lib.lg_linear_set_ffn_fused(mode)
+            try:
+                outs[mode] = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2, wp)
+            finally:
+                lib.lg_linear_set_ffn_fused(prev)
+        no_pack = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2)  # (without the packed stream: the two calls)
+        ref = _ffn_torch(x, c0, c1, w, b, ln, w2, b2)
+        torch.cuda.synchronize()
+    two, rows = outs[0].float(), outs[2].float()
+    assert torch.isfinite(rows).all()
+    d = (rows - two).abs()
+    err_rows, err_two = float((rows - ref.float()).abs().max()), float((two - ref.float()).abs().max())
+    print(f"ffn rows P={pairs} {n0}x{n1}: |rows - two| max {float(d.max()):.3e} ({int((d > 0).sum())} of {d.numel()} "
+          f"differ), vs torch: rows {err_rows:.3e}, two calls {err_two:.3e}")
+    assert bool((d <= _ulp_bound(two, x)).all()), float(d.max())
+    assert err_rows <= 2e-2 and err_two <= 2e-2
+    assert torch.equal(outs[1], outs[2] if m <= 8192 else outs[0])  # the default's choice by size
+    assert torch.equal(no_pack, outs[0]) and torch.equal(packed_c, wp)  # lg_ffn_pack == ffn_pack
 
 
 @pytest.mark.gpu

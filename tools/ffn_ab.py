@@ -1,10 +1,11 @@
-"""Diagnostic: the whole FFN in one launch (lg_linear_cat_ffn's ffn_kernel, lg_linear_set_ffn_fused(1))
-against its two calls (lg_linear_cat_ln_gelu + lg_linear(res = x), lg_linear_set_ffn_fused(0)): the op
-alone at P pairs of 1024 keypoints (graph of back-to-back calls, interleaved), then whole fp16 matcher
-forwards at P = 8 / 16 / 32 (graph replay, interleaved).
+"""A/B timing of lg_linear_cat_ffn's forms (lg_linear_set_ffn_fused: 0 its two calls, 1 by size, 2 the
+32-row one-launch ffn_rows_kernel at every size, 3 the 128-row ffn_kernel) — the op alone at P pairs of
+n keypoints (a graph of back-to-back calls per form, replays interleaved), then whole fp16 matcher
+forwards (graph replay, interleaved), with the max |difference| of each form's outputs from the first.
 
-    python tools/ffn_ab.py [lib_a.so,lib_b.so,...   (the op alone through each library: ablation builds)]
+    python tools/ffn_ab.py [--modes 0,2] [--ops 1x512,1x1024,1x2048,4x1024] [--forwards 1x512,1x1024]
 """
+import argparse
 import json
 import os
 import statistics
@@ -32,86 +33,60 @@ def replay_ms(graphs, st, reps, rounds=7):
     return {k: statistics.median(v) for k, v in times.items()}
 
 
-def op_libs(paths):
-    """The op alone at P = 16 / 32 through each library (ablation builds), interleaved."""
-    import ctypes
-    libs = []
-    for path in paths:
-        lib = ctypes.CDLL(os.path.abspath(path))
-        for name, (args, res) in list(_lib.SIGNATURES.items()) + list(_lib.HOOKS.items()):
-            if hasattr(lib, name):
-                getattr(lib, name).argtypes, getattr(lib, name).restype = args, res
-        libs.append(lib)
-    dev, dt, h, n = torch.device("cuda:0"), torch.float16, 4, 1024
-    st = torch.cuda.Stream(dev)
-    K = 20
-    for P in (16, 32):
-        M = P * 2 * n
-        x = torch.randn(1, M, 256, device=dev, dtype=dt) * 0.5
-        c0 = torch.randn(P, h, n, 64, device=dev, dtype=dt)
-        c1 = torch.randn(P, h, n, 64, device=dev, dtype=dt)
-        w, b = torch.randn(512, 512, device=dev, dtype=dt) * 0.05, torch.randn(512, device=dev, dtype=dt)
-        w2, b2 = torch.randn(256, 512, device=dev, dtype=dt) * 0.05, torch.randn(256, device=dev, dtype=dt)
-        g_, be = torch.ones(512, device=dev, dtype=dt), torch.zeros(512, device=dev, dtype=dt)
-        hb = torch.empty(1, M, 512, device=dev, dtype=dt)
-        out = torch.empty(1, M, 256, device=dev, dtype=dt)
-        graphs = {}
-        for i, lib in enumerate(libs):
-            call = lambda lib=lib: lib.lg_linear_cat_ffn(x.data_ptr(), c0.data_ptr(), c1.data_ptr(), h, n, n, P, w.data_ptr(),  # noqa: E731
-                                                         b.data_ptr(), g_.data_ptr(), be.data_ptr(), 1e-5, w2.data_ptr(),
-                                                         b2.data_ptr(), hb.data_ptr(), out.data_ptr(), st.cuda_stream)
-            with torch.cuda.stream(st):
-                assert call() == 0
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, stream=st):
-                    for _ in range(K):
-                        call()
-            graphs[os.path.basename(paths[i])] = g
-        torch.cuda.synchronize()
-        t = replay_ms(graphs, st, K)
-        print(json.dumps({"op": "ffn", "P": P, "us": {k: round(v * 1e3, 2) for k, v in t.items()}}), flush=True)
+def sizes(s):
+    return [tuple(int(v) for v in t.split("x")) for t in s.split(",") if t]
 
 
 def main():
-    if len(sys.argv) > 1:
-        return op_libs(sys.argv[1].split(","))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--modes", default="0,2")
+    ap.add_argument("--ops", default="1x512,1x1024,1x2048,2x1024,4x1024,8x1024")
+    ap.add_argument("--forwards", default="1x512,1x1024,1x2048,4x1024")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    modes = [int(m) for m in a.modes.split(",")]
     lib = _lib.load()
-    dev, dt, h, n = torch.device("cuda:0"), torch.float16, 4, 1024
+    dev, dt, h = torch.device("cuda:0"), torch.float16, 4
     st = torch.cuda.Stream(dev)
-    K = 20
+    K = a.reps
     with torch.no_grad():
-        for P in (16, 32):
+        for P, n in sizes(a.ops):
             M = P * 2 * n
-            x = torch.randn(1, M, 256, device=dev, dtype=dt) * 0.5
-            c0 = torch.randn(P, h, n, 64, device=dev, dtype=dt)
-            c1 = torch.randn(P, h, n, 64, device=dev, dtype=dt)
-            w, b = torch.randn(512, 512, device=dev, dtype=dt) * 0.05, torch.randn(512, device=dev, dtype=dt)
-            w2, b2 = torch.randn(256, 512, device=dev, dtype=dt) * 0.05, torch.randn(256, device=dev, dtype=dt)
+            gen = torch.Generator().manual_seed(P * 7 + n)
+            rnd = lambda *s: torch.randn(*s, generator=gen).to(dev, dt)  # noqa: E731
+            x = rnd(1, M, 256) * 0.5
+            c0, c1 = rnd(P, h, n, 64), rnd(P, h, n, 64)
+            w, b = rnd(512, 512) * 0.05, rnd(512) * 0.1
+            w2, b2 = rnd(256, 512) * 0.05, rnd(256) * 0.1
             ln = torch.nn.LayerNorm(512).to(dev, dt)
+            wp = mt.ffn_pack(w, w2)
             graphs, outs = {}, {}
-            for mode in (0, 1):
+            for mode in modes:
                 prev = lib.lg_linear_set_ffn_fused(mode)
                 with torch.cuda.stream(st):
-                    outs[mode] = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2)
+                    outs[mode] = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2, wp)
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, stream=st):
                         for _ in range(K):
-                            mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2)
+                            mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2, wp)
                 graphs[mode] = g
                 lib.lg_linear_set_ffn_fused(prev)
             torch.cuda.synchronize()
             t = replay_ms(graphs, st, K)
-            print(json.dumps({"op": "ffn", "P": P, "M": M, "two_calls_us": round(t[0] * 1e3, 2), "one_launch_us": round(t[1] * 1e3, 2),
-                              "bitwise_equal": bool(torch.equal(outs[0], outs[1]))}), flush=True)
+            o0 = outs[modes[0]].float()
+            print(json.dumps({"op": "ffn", "P": P, "n": n, "M": M, "us": {str(m): round(t[m] * 1e3, 2) for m in modes},
+                              "max_abs_vs_first": {str(m): float((outs[m].float() - o0).abs().max()) for m in modes}}),
+                  flush=True)
+            del graphs
 
         model = mt.LightGlueMatcher(n_layers=9).eval()
         model.load_state_dict(mt.seeded_state_dict(7, 9), strict=True)
         model = model.to(dev, dt)
-        for P in (8, 16, 32):
+        for P, n in sizes(a.forwards):
             ps = [mt.synthetic_pair(80 + i, n, n) for i in range(P)]
             pair = tuple(torch.cat([p[j] for p in ps], 0).to(dev, dt) for j in range(4))
             graphs, res = {}, {}
-            for mode in (0, 1):
+            for mode in modes:
                 prev = lib.lg_linear_set_ffn_fused(mode)
                 with torch.cuda.stream(st):
                     for _ in range(2):
@@ -124,10 +99,13 @@ def main():
                 lib.lg_linear_set_ffn_fused(prev)
             torch.cuda.synchronize()
             t = replay_ms(graphs, st, 1, rounds=21)
-            same = all(torch.equal(a, b) for a, b in zip(res[0], res[1]) if torch.is_tensor(a))
-            print(json.dumps({"forward": f"P={P}", "n": n, "ms_two_calls": round(t[0], 4), "ms_one_launch": round(t[1], 4),
-                              "pairs_per_s_two": round(P * 1e3 / t[0], 1), "pairs_per_s_one": round(P * 1e3 / t[1], 1),
-                              "outputs_bitwise_equal": same}), flush=True)
+            r0 = res[modes[0]]
+            print(json.dumps({"forward": f"P={P}", "n": n, "ms": {str(m): round(t[m], 4) for m in modes},
+                              "pairs_per_s": {str(m): round(P * 1e3 / t[m], 1) for m in modes},
+                              "desc_max_abs_vs_first": {str(m): float((res[m][0].float() - r0[0].float()).abs().max()) for m in modes},
+                              "scores_max_abs_vs_first": {str(m): float((res[m][2] - r0[2]).abs().max()) for m in modes}}),
+                  flush=True)
+            del graphs
 
 
 if __name__ == "__main__":
