@@ -54,6 +54,26 @@ def call_flops(b, h, nq, nkv, d=64):
     return 4 * b * h * nq * nkv * d
 
 
+def matcher_flops(n0, n1, pairs=1, layers=9, d=256, heads=4):
+    """Algorithmic FLOPs of one LightGlue forward as the reference computes it
+    (lightglue_pytorch_no_plugin/lightglue.py:88-233, 328-353; 2 flops per MAC; LayerNorm, GELU,
+    softmax and rotary not counted): per layer every Linear of the self block (Wqkv d->3d, out_proj
+    d->d, FFN 2d->2d and 2d->d) and the cross block (to_qk, to_v, to_out d->d, FFN) on both images'
+    M = pairs (n0 + n1) rows, = 38 M d^2, plus the four attention calls 4 H n_q n_kv 64 (self n0^2 +
+    n1^2, cross 2 n0 n1); then the head's final_proj and matchability on all rows and the similarity
+    2 n0 n1 d. (The fused path folds out_proj / to_out into the FFN's first weight: it does less work
+    than this count, which is the reference algorithm's.)"""
+    m = pairs * (n0 + n1)
+    att = 4 * heads * 64 * pairs * (n0 * n0 + n1 * n1 + 2 * n0 * n1)
+    head = 2 * m * d * d + 2 * m * d + 2 * pairs * n0 * n1 * d
+    return layers * (38 * m * d * d + att) + head
+
+
+def matcher_roofline(flops, ms):
+    tf = flops / (ms * 1e-3) / 1e12
+    return {"gflop_per_forward": round(flops / 1e9, 3), "tflops": round(tf, 2), "frac": round(tf / PEAK_F16_TFLOPS, 4)}
+
+
 def call_bytes(b, h, nq, nkv, in_bytes=2, out_bytes=2, d=64):
     return b * h * d * (nq * in_bytes + 2 * nkv * in_bytes + nq * out_bytes)
 
@@ -637,17 +657,20 @@ def matcher_attention(torch, device, stream, rank, sizes=(512, 1024, 2048), laye
     return res
 
 
-def matcher_e2e(torch, device, stream, rank, sizes=(512, 1024, 2048), reps=10):
+def matcher_e2e(torch, device, stream, rank, sizes=(512, 1024, 2048), reps=10, dtype=None):
     """BASELINE configs[3]: end-to-end LightGlue matcher latency (9 layers + final assignment,
-    fp16, seeded synthetic weights, N0 = N1 = N keypoints), one forward captured in a graph."""
+    seeded synthetic weights, N0 = N1 = N keypoints), one forward captured in a graph. fp16 (default):
+    every kernel ours; fp32 (the reference's fp32-engine mode, lightglue_attention_plugin.cpp:222-267):
+    attention through the Float boundary, projections on the framework's fp32 GEMMs."""
     from lightglue_amd import matcher
 
+    dtype = dtype or torch.float16
     model = matcher.LightGlueMatcher(n_layers=9).eval()
     model.load_state_dict(matcher.seeded_state_dict(7, 9), strict=True)
-    model = model.to(device, torch.float16)
+    model = model.to(device, dtype)
     res = {}
     for n in sizes:
-        k0, k1, d0, d1 = (t.to(device, torch.float16) for t in matcher.synthetic_pair(40 + rank, n, n))
+        k0, k1, d0, d1 = (t.to(device, dtype) for t in matcher.synthetic_pair(40 + rank, n, n))
         with torch.no_grad():
             with torch.cuda.stream(stream):
                 for _ in range(2):
@@ -667,7 +690,7 @@ def matcher_e2e(torch, device, stream, rank, sizes=(512, 1024, 2048), reps=10):
         stream.synchronize()
         ms = s_.elapsed_time(e_) / reps
         assert torch.isfinite(out[2]).all()
-        res[str(n)] = {"ms": round(ms, 4), "pairs_per_s": round(1e3 / ms, 1)}
+        res[str(n)] = {"ms": round(ms, 4), "pairs_per_s": round(1e3 / ms, 1), **matcher_roofline(matcher_flops(n, n), ms)}
     return res
 
 
@@ -710,7 +733,7 @@ def matcher_batched_pairs(torch, device, stream, rank, n=1024, pairs=(1, 4, 8, 1
         e_.record(st0)
         st0.synchronize()
         ms = s_.elapsed_time(e_) / reps
-        row = {"ms_per_forward": round(ms, 4), "pairs_per_s": round(P * 1e3 / ms, 1)}
+        row = {"ms_per_forward": round(ms, 4), "pairs_per_s": round(P * 1e3 / ms, 1), **matcher_roofline(matcher_flops(n, n, P), ms)}
         # `streams` graphs of P pairs at once (host clock, best of reps rounds)
         best = None
         for rep in range(reps + 1):
@@ -1113,6 +1136,7 @@ def main():
         result["concurrent_streams"] = concurrent_streams(torch, lightglue_amd, device, nq, nkv, rank, flops)
         result["matcher_attention"] = matcher_attention(torch, device, stream, rank, separate=args.matcher_separate)
         result["matcher_e2e_fp16"] = matcher_e2e(torch, device, stream, rank)
+        result["matcher_e2e_fp32"] = matcher_e2e(torch, device, stream, rank, dtype=torch.float32)
         result["matcher_batched_pairs_fp16"] = {"n": nq, "pairs": matcher_batched_pairs(torch, device, stream, rank, n=nq)}
         result["matcher_pair_streams_fp16"] = {"n": nq, "streams": matcher_pair_streams(torch, lightglue_amd, device,
                                                                                         rank, n=nq)}

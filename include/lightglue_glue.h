@@ -93,13 +93,12 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
 /* lg_linear_cat_ffn:    the whole FFN with the block's residual (lightglue.py:101-106, 150-151 / 174-175):
  *                       out [n0+n1, d] = x + fp16(W2 · GELU(LayerNorm(W1 · [x | merge_heads(ctx0, ctx1)] + b1)) + b2)
  *                       with d = heads*64 = 256, W1 [2d, 2d], W2 [d, 2d]. With w_packed (W1 and W2 as
- *                       lg_ffn_pack lays them out) and up to 8,192 rows (one to four image pairs of 1,024
- *                       keypoints): ONE launch, 32 rows per workgroup (ffn_rows_kernel: each wave streams
- *                       its own weight fragments into registers, the GELU output stays in LDS; within 2
- *                       fp16 ulps of the two calls). Otherwise (w_packed NULL, or more rows):
- *                       lg_linear_cat_ln_gelu into h [m, 2d] then lg_linear(h, W2, b2, res = x); see
- *                       lg_linear_set_ffn_fused. h must hold m*2d fp16 either way; out must not alias x
- *                       (16-B aligned pointers). */
+ *                       lg_ffn_pack lays them out): ONE launch, whole rows per workgroup (ffn_rows_kernel:
+ *                       32 rows up to 8,192, 64 beyond; each wave streams its own weight fragments into
+ *                       registers, the GELU output stays in LDS; within 2 fp16 ulps of the two calls).
+ *                       With w_packed NULL: lg_linear_cat_ln_gelu into h [m, 2d] then lg_linear(h, W2, b2,
+ *                       res = x). h must hold m*2d fp16 either way (unused by the one-launch form); out
+ *                       must not alias x (16-B aligned pointers). */
 int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
                           int32_t pairs, const void* w1, const void* b1, const void* gamma, const void* beta, float eps,
                           const void* w2, const void* b2, const void* w_packed, void* h, void* out, hipStream_t stream);
@@ -166,12 +165,9 @@ int32_t lg_linear_set_wide(int32_t mode);
  * round of its tiles on, 0 always two launches, 2 always one launch (A/B). The forms agree within fp16
  * rounding, not in every bit (the one-launch variance is two-pass). Returns the previous setting. */
 int32_t lg_linear_set_ln_fused(int32_t on);
-/* Test and benchmark hook for lg_linear_cat_ffn's forms: 1 (the default) by size — the one-launch
- * 32-row form up to 8,192 rows when w_packed is given, the two calls otherwise; 0 always the two
- * calls; 2 the 32-row form at every size (w_packed given); 3 the 128-row one-launch form (ffn_kernel,
- * bitwise equal to the two calls) where lg_linear_cat_ln_gelu takes its 128-row form (A/B). Values
- * outside 0..3 are clamped. Returns the previous mode. */
-int32_t lg_linear_set_ffn_fused(int32_t mode);
+/* Test and benchmark hook for lg_linear_cat_ffn's forms: 1 (the default) the one-launch form when
+ * w_packed is given, 0 always the two calls. Returns the previous setting. */
+int32_t lg_linear_set_ffn_fused(int32_t on);
 
 #ifdef __cplusplus
 }

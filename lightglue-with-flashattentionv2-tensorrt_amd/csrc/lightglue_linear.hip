@@ -42,30 +42,7 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) char lds_char;
 typedef __attribute__((address_space(3))) f16x8 lds_f16x8;
 
-// Ablation builds (tools/build_linear_variant.sh -DLG_ABL=bits; diagnostics, never shipped), in the
-// 256-row forms: 1 = no epilogue stores (the accumulators kept live), 2 = no MFMAs (nor their
-// fragment reads), 4 = no operand DMA.
-#ifndef LG_ABL
-#define LG_ABL 0
-#endif
-// (ablation build: -DLG_LN_ABL=1 drops the one-launch FFN kernel's normalisation and GELU)
-#ifndef LG_LN_KROT
-#define LG_LN_KROT 0
-#endif
-#ifndef LG_LN_AHOT
-#define LG_LN_AHOT 0
-#endif
-#ifndef LG_LN_ABL
-#define LG_LN_ABL 0
-#endif
-// (A/B build: -DLG_ST_NT=1 makes the 256-row forms' output stores non-temporal)
-#ifndef LG_ST_NT
-#define LG_ST_NT 0
-#endif
-__device__ __forceinline__ void st_out(f16* dst, f16x8 v) {
-    if constexpr (LG_ST_NT) __builtin_nontemporal_store(v, reinterpret_cast<f16x8*>(dst));
-    else *reinterpret_cast<f16x8*>(dst) = v;
-}
+__device__ __forceinline__ void st_out(f16* dst, f16x8 v) { *reinterpret_cast<f16x8*>(dst) = v; }
 constexpr int kBM = 64, kBN = 64, kKC = 128;
 // tile rows, tile channels, K columns per LDS chunk
 constexpr int kChunkBytes = 64 * kKC * 2;     // one [64 rows][128 k] fp16 chunk = 16 KiB
@@ -427,7 +404,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void linear_tile_kernel
     TileSrc<NWP, NAP> cur = src_of(0), nxt = cur;
 #pragma unroll
     for (int i = 0; i < NST - 1; ++i)
-        if constexpr (!(LG_ABL & 4)) tile_issue<GATHER, BK, KS, NT, NWV>(cur, i, smem + i * SB, wave);
+        tile_issue<GATHER, BK, KS, NT, NWV>(cur, i, smem + i * SB, wave);
 
     // fragment rows of this lane: W rows wn * WTN + 32 b + r, A rows wm * 64 + 32 b + r
     auto swz = [](int row) { return BK == 64 ? (row >> 1) & 7 : (row >> 2) & 3; };
@@ -502,8 +479,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void linear_tile_kernel
             }
             {
                 char* const fb = smem + (st == 0 ? NST - 1 : st - 1) * SB;
-                if (LG_ABL & 4) {
-                } else if (ks + NST - 1 < KS) tile_issue<GATHER, BK, KS, NT, NWV>(cur, ks + NST - 1, fb, wave);
+                if (ks + NST - 1 < KS) tile_issue<GATHER, BK, KS, NT, NWV>(cur, ks + NST - 1, fb, wave);
                 else if (more) tile_issue<GATHER, BK, KS, NT, NWV>(nxt, ks + NST - 1 - KS, fb, wave);
             }
             const unsigned sb = (unsigned)(st * SB);
@@ -521,8 +497,7 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void linear_tile_kernel
                 for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
                     for (int mb = 0; mb < 2; ++mb)
-                        if constexpr (!(LG_ABL & 2))
-                            acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[nb], af[mb], acc[nb][mb], 0, 0, 0);
+                        acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[nb], af[mb], acc[nb][mb], 0, 0, 0);
             }
         }
 
@@ -533,9 +508,6 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void linear_tile_kernel
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         lds_char* const stg = lds + st_last * SB + wave * 4096;
-        if constexpr (LG_ABL & 1) {
-            if (p.m != -12345) continue;
-        }
         const int hd = p.heads * kD;
         // Head-major outputs (QKV / SPLIT2): rows rb + 32 mb + 8 i of the coalesced phase, split
         // into (pair, row of the pair) with one division per tile and a step per row (pairs of
@@ -666,9 +638,6 @@ __device__ unsigned long long g_ln_stamps[256 * 8 * 8];
     } while (0)
 #endif
 constexpr int kLnN = 512;
-#ifndef LG_LN_2WG
-#define LG_LN_2WG 0
-#endif
 // the one-launch form's two tiles: 128 rows with 32-deep K steps through 3 stages of 40 KiB, and
 // 64 rows with 64-deep K steps through 2 stages of 72 KiB (twice the W bytes per row: it pays only
 // while the 128-row tiles would leave CUs idle; see lg_linear_cat_ln_gelu)
@@ -704,20 +673,15 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void linear_ln_kernel(L
     last_ = t_entry_;
 #endif
 
-    // (diagnostic build -DLG_LN_AHOT=1: every tile's A operand DMA'd from rows 0.., L2-hot; wrong results)
-    auto src_of = [&](int t) { return tile_src<true, BK, NWP, NAP, NWV>(p, LG_LN_AHOT ? 0 : (j0 + G * t) * MT, 0, wave, lane); };
+    auto src_of = [&](int t) { return tile_src<true, BK, NWP, NAP, NWV>(p, (j0 + G * t) * MT, 0, wave, lane); };
     // the vectors into LDS (loaded ahead of the first stages, written after them: the compiler's wait
     // counts the DMA pieces), visible after the first step's barrier
     f16x8 pv = {};
     const f16* const pvs = tid < 64 ? p.bias : tid < 128 ? gamma : beta;
     if (tid < 192) pv = *reinterpret_cast<const f16x8*>(pvs + (tid & 63) * 8);
     TileSrc<NWP, NAP> cur = src_of(0);  // (the next tile's sources are computed where used: registers)
-    // (diagnostic build -DLG_LN_KROT=1: each workgroup walks K from its own offset, so the workgroups
-    // of an XCD do not all read the same W lines at once; the same sums in another order)
-    const int krot = LG_LN_KROT ? (int)(blockIdx.x & (KS - 1)) : 0;
-    auto kstep = [&](int k) { return (k + krot) & (KS - 1); };
 #pragma unroll
-    for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, NWV>(cur, kstep(i), smem + i * SB, wave);
+    for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, NWV>(cur, i, smem + i * SB, wave);
     if (tid < 192) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
 
     auto swz = [](int row) { return BK == 64 ? (row >> 1) & 7 : (row >> 2) & 3; };
@@ -762,8 +726,8 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void linear_ln_kernel(L
             LN_SEG(1);
             {
                 char* const fb = smem + (st == 0 ? NST - 1 : st - 1) * SB;
-                if (ks + NST - 1 < KS) tile_issue<true, BK, KS, NT, NWV>(cur, kstep(ks + NST - 1), fb, wave);
-                else if (more) tile_issue<true, BK, KS, NT, NWV>(src_of(t + 1), kstep(ks + NST - 1 - KS), fb, wave);
+                if (ks + NST - 1 < KS) tile_issue<true, BK, KS, NT, NWV>(cur, ks + NST - 1, fb, wave);
+                else if (more) tile_issue<true, BK, KS, NT, NWV>(src_of(t + 1), ks + NST - 1 - KS, fb, wave);
             }
             const unsigned sb = (unsigned)(st * SB);
             st_last = st;
@@ -853,11 +817,6 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void linear_ln_kernel(L
 #pragma unroll
                         for (int u = 0; u < 4; u += 2) {
                             const f32x16& av = acc[2 * np + nbl][mb];
-                            if constexpr (LG_LN_ABL & 1) {  // (ablation: no normalisation / GELU)
-                                o[u] = (f16)av[4 * g + u];
-                                o[u + 1] = (f16)av[4 * g + u + 1];
-                                continue;
-                            }
                             const f32x2 xr = f32x2{av[4 * g + u], av[4 * g + u + 1]} * rstd;
                             const f32x2 gl = gelu_as2(f32x2{mixf<0>(xr[0], g4[u >> 1], b4[u >> 1]), mixf<1>(xr[1], g4[u >> 1], b4[u >> 1])});
                             o[u] = (f16)gl[0];
@@ -893,335 +852,77 @@ __global__ __launch_bounds__(64 * NWV, NWV == 4 ? 2 : 1) void linear_ln_kernel(L
 }
 
 
-// ---- the whole FFN with its residual in one launch (lg_linear_cat_ffn) ----
-// out = x + W2·GELU(LN(W1·[x | heads] + b1)) + b2 (lightglue.py:101-106 and the blocks' residual,
-// :150-151 / :174-175). Phase 1 is linear_ln_kernel<16, 128, 32, 3> (128-row tiles owning whole
-// rows); its fp16 GELU output h stays in LDS (128 KiB, [row][512] with 16-B chunks XOR-swizzled by
-// row & 7: conflict-free fragment reads) instead of going to HBM and back. Phase 2: 8 waves as 2 (m)
-// x 4 (n) tiles of 64 x 64 of the 128 x 256 output, K = 512 in 16-deep MFMA steps whose W2
-// fragments come from global memory (256 KiB, L2-resident) straight into registers kFfnPf steps
-// ahead; then fp16(acc + b2) + x, staged through LDS and stored as whole 128-B row segments — the
-// operations of lg_linear_cat_ln_gelu + lg_linear(res = x) in the same order (bitwise equal). Each
-// tile starts its ring afresh (the next tile's first K steps would land in LDS that h occupies).
-// (ablation builds, -DLG_FFN_ABL=bits, wrong results: 1 no W2 loads in phase 2, 2 no phase-2 MFMAs,
-// 4 no phase-2 epilogue (residual loads, stores), 8 no phase 2 at all)
-#ifndef LG_FFN_ABL
-#define LG_FFN_ABL 0
-#endif
 constexpr int kFfnOut = 256;  // the FFN's output channels (d)
-#ifndef LG_FFN_PF
-#define LG_FFN_PF 8
-#endif
-constexpr int kFfnPf = LG_FFN_PF;  // W2 fragment steps in flight per wave (A/B: -DLG_FFN_PF)
-__global__ __launch_bounds__(512, 1) void ffn_kernel(LinArgs p, const f16* __restrict__ gamma, const f16* __restrict__ beta,
-                                                     float eps, const f16* __restrict__ w2, const f16* __restrict__ b2) {
-    constexpr int KS = 16, MT = 128, BK = 32, NST = 3, NT = kLnN;
-    constexpr int WM = 2, WN = 4, WTN = NT / WN, NB = WTN / 32, NP = WTN / 64;
-    constexpr int SB = (MT + NT) * BK * 2;                             // 40 KiB ring stages
-    constexpr int NWP = NT * BK * 2 / 8192, NAP = MT * BK * 2 / 8192;  // 4 + 1 pieces per wave and step
-    constexpr int D = NWP + NAP;
-    constexpr int kH = 0;                         // h [128][512] fp16 (over the ring, after phase 1)
-    constexpr int kPar = MT * NT * 2;             // b1, gamma, beta [512] fp16
-    constexpr int kRed = kPar + 3 * NT * 2;       // row partials [2][MT][WN] fp32
-    static_assert(NST * SB <= kPar && (NST - 2) * D <= 63, "shape");
-    __shared__ __attribute__((aligned(16))) char smem[kRed + 2 * MT * WN * 4];
-    lds_char* const lds = (lds_char*)smem;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave % WM, wn = wave / WM;
-    const int r = lane & 31, hh = lane >> 5;
-    const int T = p.total, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
-    const int q8 = T >> 3, r8 = T & 7;
-    const int jb = xcd * q8 + min(xcd, r8), je = jb + q8 + (xcd < r8 ? 1 : 0);
-    const int G = ((int)gridDim.x - xcd + 7) >> 3;
-    const int j0 = jb + loc;
-    if (j0 >= je) return;
-    const int ntile_w = (je - j0 + G - 1) / G;
 
-    auto src_of = [&](int t) { return tile_src<true, BK, NWP, NAP, 8>(p, (j0 + G * t) * MT, 0, wave, lane); };
-    f16x8 pv = {};
-    const f16* const pvs = tid < 64 ? p.bias : tid < 128 ? gamma : beta;
-    if (tid < 192) pv = *reinterpret_cast<const f16x8*>(pvs + (tid & 63) * 8);
-    TileSrc<NWP, NAP> cur = src_of(0);
-#pragma unroll
-    for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, 8>(cur, i, smem + i * SB, wave);
-    if (tid < 192) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
-
-    auto swz = [](int row) { return (row >> 2) & 3; };
-    unsigned wro[NB], aro[2];
-    int wsw[NB], asw[2];
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-        const int wrow = wn * WTN + 32 * b + r;
-        wro[b] = (unsigned)(wrow * BK * 2), wsw[b] = swz(wrow);
-    }
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-        const int arow = wm * 64 + 32 * b + r;
-        aro[b] = (unsigned)(NT * BK * 2 + arow * BK * 2), asw[b] = swz(arow);
-    }
-    const int cr = lane >> 3, cc = lane & 7;
-    float* const red = (float*)(void*)(smem + kRed);  // [pass][row][wn]
-    auto red_sum = [&](int off) {
-        float v = 0.f;
-#pragma unroll
-        for (int q = 0; q < WN; q += 4) {
-            const f32x4 w4 = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (off + q) * 4);
-            v += (w4[0] + w4[1]) + (w4[2] + w4[3]);
-        }
-        return v;
-    };
-    // phase 2's W2 fragments: lane (r, hh) of n-block nb reads row wn * 64 + 32 nb + r, k 16 j + 8 hh
-    // (a buffer descriptor: one lane offset, the step's offset a scalar constant)
-    const __amdgpu_buffer_rsrc_t w2rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(w2), (short)0, kFfnOut * NT * 2, 0x00020000);
-    const unsigned w2lo = (unsigned)(((wn * 64 + r) * NT + 8 * hh) * 2);
-    auto w2frag = [&](int nb, int j) {
-        if constexpr (LG_FFN_ABL & 1) {
-            unsigned z0, z1, z2, z3, src = w2lo + (unsigned)j;
-            asm volatile("v_mov_b32 %0, %4\n\tv_mov_b32 %1, %4\n\tv_mov_b32 %2, %4\n\tv_mov_b32 %3, %4"
-                         : "=v"(z0), "=v"(z1), "=v"(z2), "=v"(z3) : "v"(src));
-            typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
-            return __builtin_bit_cast(f16x8, u32x4_{z0, z1, z2, z3 + (unsigned)nb});
-        }
-        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(w2rs, w2lo, (32 * nb * NT + 16 * j) * 2, 0));
-    };
-    for (int t = 0; t < ntile_w; ++t) {
-        const int m0 = (j0 + G * t) * MT;
-        if (t > 0) {  // a fresh ring (the previous tile's output stores drained first: exact counts)
-            cur = src_of(t);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-            for (int i = 0; i < NST - 1; ++i) tile_issue<true, BK, KS, NT, 8>(cur, i, smem + i * SB, wave);
-        }
-        f32x16 acc[NB][2] = {};
-        int st = 0;
-#pragma unroll 2
-        for (int ks = 0; ks < KS; ++ks) {
-            if (ks + NST - 2 > KS - 1) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NST - 2) * D) : "memory");
-            __builtin_amdgcn_s_barrier();
-            if (ks + NST - 1 < KS) tile_issue<true, BK, KS, NT, 8>(cur, ks + NST - 1, smem + (st == 0 ? NST - 1 : st - 1) * SB, wave);
-            const unsigned sb = (unsigned)(st * SB);
-            st = st == NST - 1 ? 0 : st + 1;
-#pragma unroll
-            for (int s = 0; s < BK / 16; ++s) {
-                const int u = 2 * s + hh;
-                f16x8 wf[NB], af[2];
-#pragma unroll
-                for (int b = 0; b < NB; ++b) wf[b] = *(lds_f16x8*)(lds + sb + wro[b] + ((u ^ wsw[b]) << 4));
-#pragma unroll
-                for (int b = 0; b < 2; ++b) af[b] = *(lds_f16x8*)(lds + sb + aro[b] + ((u ^ asw[b]) << 4));
-#pragma unroll
-                for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-                    for (int mb = 0; mb < 2; ++mb)
-                        acc[nb][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wf[nb], af[mb], acc[nb][mb], 0, 0, 0);
-            }
-        }
-        // ---- h = GELU(LN(fp16(acc + b1))) as linear_ln_kernel computes it, into the h region ----
-        const int nw0 = wn * WTN;
-        float rs[2];
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            float s = 0.f;
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const u32x2 b4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + (nw0 + 32 * nb + 8 * g + 4 * hh) * 2);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const float a = acc[nb][mb][4 * g + u];
-                        const float h = (u & 1) ? mixh<1>(a, b4[u >> 1]) : mixh<0>(a, b4[u >> 1]);
-                        acc[nb][mb][4 * g + u] = h;
-                        s += h;
-                    }
-                }
-            rs[mb] = s + __shfl_xor(s, 32, 64);
-        }
-        if (hh == 0) {
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb) red[(wm * 64 + 32 * mb + r) * WN + wn] = rs[mb];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        float mean[2];
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            mean[mb] = red_sum((wm * 64 + 32 * mb + r) * WN) * (1.f / kLnN);
-            float q = 0.f;
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    const float d = acc[nb][mb][e] - mean[mb];
-                    acc[nb][mb][e] = d;
-                    q = __builtin_fmaf(d, d, q);
-                }
-            rs[mb] = q + __shfl_xor(q, 32, 64);
-        }
-        if (hh == 0) {
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb) red[MT * WN + (wm * 64 + 32 * mb + r) * WN + wn] = rs[mb];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // (also: every wave is done reading the ring, which h overwrites)
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-            const int row = wm * 64 + 32 * mb + r;  // tile row of this lane
-            const float rstd = __builtin_amdgcn_rsqf(red_sum(MT * WN + row * WN) * (1.f / kLnN) + eps);
-#pragma unroll
-            for (int np = 0; np < NP; ++np)
-#pragma unroll
-                for (int nbl = 0; nbl < 2; ++nbl)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const int n = nw0 + 64 * np + 32 * nbl + 8 * g + 4 * hh;
-                        const u32x2 g4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + NT * 2 + n * 2);
-                        const u32x2 b4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + 2 * NT * 2 + n * 2);
-                        f16x4 o;
-#pragma unroll
-                        for (int u = 0; u < 4; u += 2) {
-                            const f32x16& av = acc[2 * np + nbl][mb];
-                            const f32x2 xr = f32x2{av[4 * g + u], av[4 * g + u + 1]} * rstd;
-                            const f32x2 gl = gelu_as2(f32x2{mixf<0>(xr[0], g4[u >> 1], b4[u >> 1]), mixf<1>(xr[1], g4[u >> 1], b4[u >> 1])});
-                            o[u] = (f16)gl[0];
-                            o[u + 1] = (f16)gl[1];
-                        }
-                        *(__attribute__((address_space(3))) f16x4*)(lds + kH + row * (NT * 2) + (((n >> 3) ^ (row & 7)) << 4) + 8 * hh) = o;
-                    }
-        }
-        // the first W2 fragments in flight across the barrier (the phase-1 accumulators are dead here)
-        f16x8 wq[kFfnPf][2];
-#pragma unroll
-        for (int j = 0; j < kFfnPf; ++j)
-#pragma unroll
-            for (int nb = 0; nb < 2; ++nb) wq[j][nb] = w2frag(nb, j);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // h complete
-        if constexpr (LG_FFN_ABL & 8) continue;
-        // ---- phase 2: out tile [wm * 64, +64) x [wn * 64, +64) = h · W2ᵀ, K in 16-deep steps ----
-        f32x16 o2[2][2] = {};
-#pragma unroll 1
-        for (int jb2 = 0; jb2 < KS * 2; jb2 += kFfnPf)
-#pragma unroll
-        for (int jj = 0; jj < kFfnPf; ++jj) {
-            const int j = jb2 + jj;
-            const f16x8 w0 = wq[jj][0], w1 = wq[jj][1];
-            if (j + kFfnPf < KS * 2) {
-#pragma unroll
-                for (int nb = 0; nb < 2; ++nb) wq[jj][nb] = w2frag(nb, j + kFfnPf);
-            }
-            f16x8 hf[2];
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb) {
-                const int row = wm * 64 + 32 * mb + r;
-                hf[mb] = *(lds_f16x8*)(lds + kH + row * (NT * 2) + (((2 * j + hh) ^ (row & 7)) << 4));
-            }
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb) {
-                if constexpr (LG_FFN_ABL & 2) {
-                    asm volatile("" ::"v"(w0), "v"(w1), "v"(hf[mb]));
-                    continue;
-                }
-                o2[0][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w0, hf[mb], o2[0][mb], 0, 0, 0);
-                o2[1][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w1, hf[mb], o2[1][mb], 0, 0, 0);
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // every wave is done reading h: its region stages the output
-        if constexpr (LG_FFN_ABL & 4) {
-            asm volatile("" ::"v"(o2[0][0]), "v"(o2[0][1]), "v"(o2[1][0]), "v"(o2[1][1]));
-            continue;
-        }
-        // ---- out = fp16(fp16(acc + b2) + x): 32 rows x 64 channels a round through this wave's 4 KiB ----
-        lds_char* const stg = lds + kH + wave * 4096;
-        const int c0 = wn * 64;
-        u32x2 bb[2][4];
-#pragma unroll
-        for (int nbl = 0; nbl < 2; ++nbl)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) bb[nbl][g] = *reinterpret_cast<const u32x2*>(b2 + c0 + 32 * nbl + 8 * g + 4 * hh);
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-#pragma unroll
-            for (int nbl = 0; nbl < 2; ++nbl)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const f32x16& a = o2[nbl][mb];
-                    const f16x4 b4 = __builtin_bit_cast(f16x4, bb[nbl][g]);
-                    const f16x4 v = f16x4{lin_val(a[4 * g], b4[0]), lin_val(a[4 * g + 1], b4[1]),
-                                          lin_val(a[4 * g + 2], b4[2]), lin_val(a[4 * g + 3], b4[3])};
-                    *(__attribute__((address_space(3))) f16x4*)(stg + r * 128 + (((4 * nbl + g) ^ (r & 7)) << 4) + 8 * hh) = v;
-                }
-            f16x8 o[4], xr[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int rl = 8 * i + cr;
-                o[i] = *(lds_f16x8*)(stg + rl * 128 + ((cc ^ (rl & 7)) << 4));
-                const int row = min(m0 + wm * 64 + 32 * mb + rl, p.m - 1);
-                xr[i] = *reinterpret_cast<const f16x8*>(p.a + (size_t)row * (p.k / 2) + c0 + 8 * cc);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int row = min(m0 + wm * 64 + 32 * mb + 8 * i + cr, p.m - 1);
-                f16x8 v = o[i];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], xr[i][e]);
-                st_out(p.out[0] + (size_t)row * kFfnOut + c0 + 8 * cc, v);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the next round rewrites stg)
-        }
-        __builtin_amdgcn_s_barrier();  // (the next tile's ring overwrites the staging regions)
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// ---- the whole FFN for launches of few rows (lg_linear_cat_ffn at P = 1..4 pairs, round 6) ----
-// out = x + fp16(W2 · GELU(LN(fp16(W1 · [x | heads] + b1))) + b2) with one workgroup per 32 rows: at
-// a single image pair (M = 1,024..4,096) the FFN was three launches of ~5 us each, every one of them
-// near the launch floor (profiles/r05/single_pair_timelines.txt: 269 of 557 us of a forward at n =
-// 1,024). Here one launch: 8 waves, wave w owns hidden channels [64w, 64w + 64) in phase 1 and output
+// ---- the whole FFN in one launch, whole rows per workgroup (lg_linear_cat_ffn, round 6) ----
+// out = x + fp16(W2 · GELU(LN(fp16(W1 · [x | heads] + b1))) + b2) with one workgroup per MT = 32 MB rows.
+// At a single image pair (M = 1,024..4,096) the FFN was three launches of ~5 us each, every one near
+// the launch floor (profiles/r05/single_pair_timelines.txt: 269 of 557 us of a forward at n = 1,024).
+// Here one launch: 8 waves, wave w owns hidden channels [64w, 64w + 64) in phase 1 and output
 // channels [32w, 32w + 32) in phase 2, so every weight fragment a wave multiplies is its own — W1 and
 // W2 stream from L2 straight into VGPRs in the MFMA A-operand layout (lane (r, hh): row r of the
-// wave's 32-channel block, k = 16 s + 8 hh .. + 8 of step s; lg_ffn_pack stores them in that order),
-// D steps ahead, as ONE stream that runs from phase 1 into phase 2 (W2's first fragments load under
-// the LayerNorm); no barrier in either GEMM loop. The 32 activation rows [x | heads] (the A-gather of lg_linear_cat) sit in LDS for the
-// whole launch (32 KiB, rows of 1 KiB with 16-B units XOR (row & 15): conflict-free ds_read_b128 of
-// 16 rows at one k), as does GELU's output h (the second GEMM's B operand, the same layout), and the
-// residual x is read back from the A tile. Per workgroup the weights are 768 KiB, the bound of this
-// form (~12 k cycles at the ~64 B/clk a CU takes in), whatever the rows per workgroup: 32 rows keep
-// the MFMA work (6 k cycles per SIMD) under it with the fewest workgroups re-reading W.
-// Arithmetic: h = fp16(acc + b1) and the output fp16(fp16(acc + b2) + x) as lin_val / res_add (the
-// k16 blocks in the 64 x 64 form's order: h before the LayerNorm and the second product given h are
-// bitwise those of the two-call path); LayerNorm two-pass over the row's 512 values (mean, then the
-// sum of squared deviations; fixed reduction order), normalisation and GELU as linear_ln_kernel.
-constexpr int kFrMT = 32;             // rows per workgroup
-constexpr int kFrMaxRows = 256 * kFrMT;  // the by-size choice: one round of workgroups (8,192 rows)
+// wave's 32-channel block, k = 16 s + 8 hh .. + 8 of step s; lg_ffn_pack stores them in that order,
+// so every load is one contiguous KiB), D steps ahead, as ONE stream that runs from phase 1 into
+// phase 2 (W2's first fragments load under the LayerNorm); no barrier in either GEMM loop. The MT
+// activation rows [x | heads] (the A-gather of lg_linear_cat) sit in LDS for the whole launch (rows of
+// 1 KiB with 16-B units XOR (row & 15): conflict-free ds_read_b128 of 16 rows at one k), as does GELU's
+// output h (the second GEMM's B operand, the same layout); the residual x is read back from the A tile.
+// Per workgroup the weights are 768 KiB whatever MT (~12 k cycles at the ~64 B/clk a CU takes in):
+// MT = 32 (MB = 1) gives the most workgroups for a few rows (latency: single pairs), MT = 64 (MB = 2)
+// halves the weight bytes per row where there are rows enough for several rounds (its MFMA work,
+// 12 k cycles per SIMD, then matches the stream).
+// Arithmetic: the k16 blocks in the 64 x 64 form's order; h = fp16(acc + b1) in one rounding, the
+// LayerNorm statistics as lg_layernorm_gelu forms them (sum and sum of squares, fixed reduction order),
+// normalisation and GELU as linear_ln_kernel, the output fp16(fp16(acc + b2) + x) as lin_val / res_add.
 constexpr int kFfnPackedBytes = (512 * 512 + 256 * 512) * 2;  // lg_ffn_pack: 8 wave streams of 96 KiB
-template <int D>
+// Diagnostic build (-DLG_FR_STAMPS, tools/fr_stamps.py; never shipped): per wave of the first 256
+// workgroups, s_memtime cycles of chained segments (0 entry -> A in LDS, 1 phase 1, 2 LayerNorm + GELU,
+// 3 phase 2, 4 epilogue), read back by lg_diag_fr_stamps.
+#ifdef LG_FR_STAMPS
+__device__ unsigned long long g_fr_stamps[256 * 8 * 8];
+#define FR_SEG(k)                                                                                    \
+    do {                                                                                             \
+        unsigned long long t_;                                                                       \
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        fr_[k] = t_ - fr_last_;                                                                      \
+        fr_last_ = t_;                                                                               \
+    } while (0)
+#else
+#define FR_SEG(k) \
+    do {          \
+    } while (0)
+#endif
+template <int MB, int D>
 __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* __restrict__ gamma,
                                                           const f16* __restrict__ beta, float eps,
                                                           const f16* __restrict__ wp, const f16* __restrict__ b2) {
+    constexpr int MT = 32 * MB;                    // rows per workgroup
     constexpr int K = 512, NO = kFfnOut;           // FFN width (= hidden), output channels
-    constexpr int kA = 0, kH = kFrMT * K * 2;      // A and h tiles, [32][1 KiB] each
-    constexpr int kStg = 2 * kH;                   // output staging, 2.5 KiB per wave ([32][80 B])
-    constexpr int kPar = kStg + 8 * kFrMT * 80;    // b1, gamma, beta [512], b2 [256] fp16
-    constexpr int kRed = kPar + (3 * K + NO) * 2;  // row partials [2][32][8 waves] fp32
+    constexpr int kA = 0, kH = MT * K * 2;         // A and h tiles, [MT][1 KiB] each
+    constexpr int kSP = 80;                        // output staging pitch (64 B of a row + 16)
+    constexpr int kStg = MB == 1 ? 2 * kH : kH;    // staging: its own region (MB = 1), else over h
+    constexpr int kPar = MB == 1 ? kStg + 8 * MT * kSP : 2 * kH;  // b1, gamma, beta [512], b2 [256] fp16
+    constexpr int kRed = kPar + (3 * K + NO) * 2;  // row partials [2][MT][8 waves] fp32
     constexpr int NS1 = K / 16, NS = 2 * NS1;      // k16 steps per GEMM; the stream: phase 1, then 2
-    static_assert(D >= 1 && D <= NS1, "prefetch depth");
-    __shared__ __attribute__((aligned(16))) char smem[kRed + 2 * kFrMT * 8 * 4];
+    static_assert(D >= 1 && D <= NS1 && (MB == 1 || MB == 2), "shape");
+    static_assert(MB == 1 || 8 * MT * kSP <= kH, "staging over h");
+    __shared__ __attribute__((aligned(16))) char smem[kRed + 2 * MT * 8 * 4];
     lds_char* const lds = (lds_char*)smem;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, hh = lane >> 5;
-    const int m0 = blockIdx.x * kFrMT;
+    const int m0 = blockIdx.x * MT;
+#ifdef LG_FR_STAMPS
+    unsigned long long fr_[6] = {0, 0, 0, 0, 0, 0}, fr_last_, fr_entry_;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fr_entry_)::"memory");
+    fr_last_ = fr_entry_;
+#endif
 
     // ---- A tile: row 8 i + wave, 16-B unit `lane` (x: units 0..31, head h of the attention output:
     // units 32 + 8 h .. + 7), loaded whole-row coalesced; rows past m repeat row m - 1 ----
-    f16x8 av[4];
+    f16x8 av[4 * MB];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4 * MB; ++i) {
         const int grow = min(m0 + 8 * i + wave, p.m - 1);
         const f16* src;
         if (lane < 32) {
@@ -1238,6 +939,10 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
         const f16* const pvs = tid < 64 ? p.bias : tid < 128 ? gamma : tid < 192 ? beta : b2;
         pv = *reinterpret_cast<const f16x8*>(pvs + (tid & 63) * 8);
     }
+
+    // every wave's A loads are issued before any wave's weight stream: the loads of a CU pass its
+    // texture unit in issue order, and A behind seven waves' weight prefetch waited ~2.6 k cycles
+    asm volatile("s_barrier" ::: "memory");
 
     // ---- the weight stream (lg_ffn_pack's layout): wave w's 96 KiB, piece i at w * 96 KiB + i KiB,
     // lane l's 16 B at + 16 l: step j of phase 1, block b = piece 2 j + b; step j of phase 2 = 64 + j.
@@ -1258,22 +963,32 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
     }
     // A and the vectors into LDS (the compiler's wait counts the weight loads issued after them)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4 * MB; ++i) {
         const int row = 8 * i + wave;
         *(lds_f16x8*)(lds + kA + row * 1024 + ((lane ^ (row & 15)) << 4)) = av[i];
     }
     if (tid < 224) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    FR_SEG(0);
 
-    // B-operand fragment of step s from a [32][1 KiB] tile: row r, unit 2 s + hh
-    auto bfrag = [&](int base, int s) {
-        return *(lds_f16x8*)(lds + base + r * 1024 + (((2 * s + hh) ^ (r & 15)) << 4));
+    // B-operand fragments of step s from an [MT][1 KiB] tile: rows 32 mb + r, unit 2 s + hh
+    struct BF {
+        f16x8 v[MB];
     };
-    // ---- phase 1: hᵀ (the wave's 64 channels x 32 rows) = W1 · Aᵀ ----
-    // (each step's B fragment is read one step ahead: its LDS latency under the previous MFMAs)
-    f32x16 acc[2] = {};
-    f16x8 af = bfrag(kA, 0);
+    auto bfrag = [&](int base, int s) {
+        BF f;
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+            const int row = 32 * mb + r;
+            f.v[mb] = *(lds_f16x8*)(lds + base + row * 1024 + (((2 * s + hh) ^ (row & 15)) << 4));
+        }
+        return f;
+    };
+    // ---- phase 1: hᵀ (the wave's 64 channels x MT rows) = W1 · Aᵀ; each step's B fragments are read
+    // one step ahead (their LDS latency under the previous MFMAs) ----
+    f32x16 acc[2][MB] = {};
+    BF af = bfrag(kA, 0);
 #pragma unroll
     for (int j = 0; j < NS1; ++j) {
         const f16x8 wa = q[j % D][0], wb = q[j % D][1];
@@ -1281,110 +996,144 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
             q[j % D][0] = wfrag(j + D, 0);
             if (j + D < NS1) q[j % D][1] = wfrag(j + D, 1);
         }
-        const f16x8 an = j + 1 < NS1 ? bfrag(kA, j + 1) : af;
-        acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa, af, acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wb, af, acc[1], 0, 0, 0);
+        const BF an = j + 1 < NS1 ? bfrag(kA, j + 1) : af;
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+            acc[0][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa, af.v[mb], acc[0][mb], 0, 0, 0);
+            acc[1][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wb, af.v[mb], acc[1][mb], 0, 0, 0);
+        }
         af = an;
         __builtin_amdgcn_sched_barrier(0);
     }
 
-    // ---- LayerNorm over the row's 512 h values: the wave's 64 are in lanes r and r + 32 ----
-    // lane (r, hh): acc[b][4 g + t] = hidden channel 64 w + 32 b + 8 g + 4 hh + t of row m0 + r
+    FR_SEG(1);
+    // ---- LayerNorm over each row's 512 h values: the wave's 64 are in lanes r and r + 32 ----
+    // lane (r, hh): acc[b][mb][4 g + t] = hidden channel 64 w + 32 b + 8 g + 4 hh + t of row 32 mb + r.
+    // h = fp16(acc + b1) in one rounding (v_fma_mixlo_f16; the two calls' lin_val rounds through fp32
+    // first: the same value but for a rare double rounding), then the row's sum and sum of squares
+    // in one pass and mean / variance as lg_layernorm_gelu forms them (E[h^2] - mean^2, fp32): one
+    // exchange through LDS (vector issue bounds this phase: ~19 VALU per value, two waves a SIMD)
     float* const red = (float*)(void*)(smem + kRed);  // [pass][row][wave]
-    float s = 0.f;
+    float sm[MB], sq[MB];
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int mb = 0; mb < MB; ++mb) {
+        float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + (64 * wave + 32 * b + 8 * g + 4 * hh) * 2);
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const float h = (float)lin_val(acc[b][4 * g + t], b4[t]);
-                acc[b][4 * g + t] = h;
-                s += h;
+            for (int g = 0; g < 4; ++g) {
+                const u32x2 b4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + (64 * wave + 32 * b + 8 * g + 4 * hh) * 2);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const float h = (t & 1) ? mixh<1>(acc[b][mb][4 * g + t], b4[t >> 1]) : mixh<0>(acc[b][mb][4 * g + t], b4[t >> 1]);
+                    acc[b][mb][4 * g + t] = h;
+                    s1 += h;
+                    s2 = __builtin_fmaf(h, h, s2);
+                }
             }
+        sm[mb] = s1 + __shfl_xor(s1, 32, 64);
+        sq[mb] = s2 + __shfl_xor(s2, 32, 64);
+    }
+    if (hh == 0) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+            red[(32 * mb + r) * 8 + wave] = sm[mb];
+            red[MT * 8 + (32 * mb + r) * 8 + wave] = sq[mb];
         }
-    s += __shfl_xor(s, 32, 64);
-    if (hh == 0) red[r * 8 + wave] = s;
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    auto row_sum = [&](int off) {  // the 8 waves' partials of row r, in a fixed order
-        const f32x4 a = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (off + r * 8) * 4);
-        const f32x4 c = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (off + r * 8 + 4) * 4);
+    auto row_sum = [&](int off, int row) {  // the 8 waves' partials of a row, in a fixed order
+        const f32x4 a = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (off + row * 8) * 4);
+        const f32x4 c = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (off + row * 8 + 4) * 4);
         return ((a[0] + a[1]) + (a[2] + a[3])) + ((c[0] + c[1]) + (c[2] + c[3]));
     };
-    const float mean = row_sum(0) * (1.f / K);
-    float qv = 0.f;
+    // GELU(LN(h)) -> fp16 into the h tile (unit 8 w + 4 b + g of the row, half hh)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int mb = 0; mb < MB; ++mb) {
+        const int row = 32 * mb + r;
+        const float mean = row_sum(0, row) * (1.f / K);
+        const float rstd = __builtin_amdgcn_rsqf(fmaxf(row_sum(MT * 8, row) * (1.f / K) - mean * mean, 0.f) + eps);
+        const float nmr = -mean * rstd;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const float d = acc[b][e] - mean;
-            acc[b][e] = d;
-            qv = __builtin_fmaf(d, d, qv);
-        }
-    qv += __shfl_xor(qv, 32, 64);
-    if (hh == 0) red[kFrMT * 8 + r * 8 + wave] = qv;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const float rstd = __builtin_amdgcn_rsqf(row_sum(kFrMT * 8) * (1.f / K) + eps);
-    // GELU(LN(h)) -> fp16 into the h tile (unit 8 w + 4 b + g of row r, half hh)
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+            for (int g = 0; g < 4; ++g) {
+                const int n = 64 * wave + 32 * b + 8 * g + 4 * hh;
+                const u32x2 g4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + K * 2 + n * 2);
+                const u32x2 be4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + 2 * K * 2 + n * 2);
+                f16x4 o;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int n = 64 * wave + 32 * b + 8 * g + 4 * hh;
-            const u32x2 g4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + K * 2 + n * 2);
-            const u32x2 be4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + 2 * K * 2 + n * 2);
-            f16x4 o;
-#pragma unroll
-            for (int u = 0; u < 4; u += 2) {
-                const f32x2 xr = f32x2{acc[b][4 * g + u], acc[b][4 * g + u + 1]} * rstd;
-                const f32x2 gl = gelu_as2(f32x2{mixf<0>(xr[0], g4[u >> 1], be4[u >> 1]), mixf<1>(xr[1], g4[u >> 1], be4[u >> 1])});
-                o[u] = (f16)gl[0];
-                o[u + 1] = (f16)gl[1];
+                for (int u = 0; u < 4; u += 2) {
+                    const f32x2 xr = f32x2{acc[b][mb][4 * g + u], acc[b][mb][4 * g + u + 1]} * rstd + nmr;
+                    const f32x2 gl = gelu_as2(f32x2{mixf<0>(xr[0], g4[u >> 1], be4[u >> 1]), mixf<1>(xr[1], g4[u >> 1], be4[u >> 1])});
+                    o[u] = (f16)gl[0];
+                    o[u + 1] = (f16)gl[1];
+                }
+                *(__attribute__((address_space(3))) f16x4*)(lds + kH + row * 1024 + (((8 * wave + 4 * b + g) ^ (row & 15)) << 4) + 8 * hh) = o;
             }
-            *(__attribute__((address_space(3))) f16x4*)(lds + kH + r * 1024 + (((8 * wave + 4 * b + g) ^ (r & 15)) << 4) + 8 * hh) = o;
-        }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // h complete
+    FR_SEG(2);
 
-    // ---- phase 2: outᵀ (the wave's 32 channels x 32 rows) = W2 · hᵀ ----
-    f32x16 o2 = {};
-    f16x8 hf = bfrag(kH, 0);
+    // ---- phase 2: outᵀ (the wave's 32 channels x MT rows) = W2 · hᵀ ----
+    f32x16 o2[MB] = {};
+    BF hf = bfrag(kH, 0);
 #pragma unroll
     for (int j = NS1; j < NS; ++j) {
         const f16x8 wa = q[j % D][0];
         if (j + D < NS) q[j % D][0] = wfrag(j + D, 0);
-        const f16x8 hn = j + 1 < NS ? bfrag(kH, j + 1 - NS1) : hf;
-        o2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa, hf, o2, 0, 0, 0);
+        const BF hn = j + 1 < NS ? bfrag(kH, j + 1 - NS1) : hf;
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) o2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa, hf.v[mb], o2[mb], 0, 0, 0);
         hf = hn;
         __builtin_amdgcn_sched_barrier(0);
     }
-
-    // ---- out = fp16(fp16(acc + b2) + x): the wave's 32 x 32 block staged row-major in its own LDS
-    // rows (80-B pitch), then two lanes a row, 32 B each, with x from the A tile ----
-    lds_char* const stg = lds + kStg + wave * (kFrMT * 80);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const int c = 32 * wave + 8 * g + 4 * hh;
-        const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + 3 * K * 2 + c * 2);
-        const f16x4 v = f16x4{lin_val(o2[4 * g], b4[0]), lin_val(o2[4 * g + 1], b4[1]), lin_val(o2[4 * g + 2], b4[2]),
-                              lin_val(o2[4 * g + 3], b4[3])};
-        *(__attribute__((address_space(3))) f16x4*)(stg + r * 80 + (8 * g + 4 * hh) * 2) = v;
+    FR_SEG(3);
+    if constexpr (MB > 1) {  // (the staging rows lie over h: every wave done reading it)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
     }
+
+    // ---- out = fp16(fp16(acc + b2) + x): the wave's MT x 32 block staged row-major in its own LDS
+    // rows (80-B pitch), then two lanes a row, 32 B each, with x from the A tile ----
+    lds_char* const stg = lds + kStg + wave * (MT * kSP);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int c = 32 * wave + 8 * g + 4 * hh;
+            const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + 3 * K * 2 + c * 2);
+            const f16x4 v = f16x4{lin_val(o2[mb][4 * g], b4[0]), lin_val(o2[mb][4 * g + 1], b4[1]),
+                                  lin_val(o2[mb][4 * g + 2], b4[2]), lin_val(o2[mb][4 * g + 3], b4[3])};
+            *(__attribute__((address_space(3))) f16x4*)(stg + (32 * mb + r) * kSP + (8 * g + 4 * hh) * 2) = v;
+        }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the wave's own rows: LDS ops of a wave in order)
-    const int rr = lane >> 1, half = lane & 1;
-    if (m0 + rr < p.m) {
 #pragma unroll
-        for (int e2 = 0; e2 < 2; ++e2) {
-            f16x8 v = *(lds_f16x8*)(stg + rr * 80 + half * 32 + e2 * 16);
-            const f16x8 xr = *(lds_f16x8*)(lds + kA + rr * 1024 + (((4 * wave + 2 * half + e2) ^ (rr & 15)) << 4));
+    for (int mb = 0; mb < MB; ++mb) {
+        const int rr = 32 * mb + (lane >> 1), half = lane & 1;
+        if (m0 + rr < p.m) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], xr[e]);
-            *reinterpret_cast<f16x8*>(p.out[0] + (size_t)(m0 + rr) * NO + 32 * wave + 16 * half + 8 * e2) = v;
+            for (int e2 = 0; e2 < 2; ++e2) {
+                f16x8 v = *(lds_f16x8*)(stg + rr * kSP + half * 32 + e2 * 16);
+                const f16x8 xr = *(lds_f16x8*)(lds + kA + rr * 1024 + (((4 * wave + 2 * half + e2) ^ (rr & 15)) << 4));
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], xr[e]);
+                *reinterpret_cast<f16x8*>(p.out[0] + (size_t)(m0 + rr) * NO + 32 * wave + 16 * half + 8 * e2) = v;
+            }
         }
     }
+#ifdef LG_FR_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FR_SEG(4);
+    if (lane == 0 && blockIdx.x < 256) {
+        unsigned long long* d = g_fr_stamps + ((size_t)blockIdx.x * 8 + wave) * 8;
+        for (int k = 0; k < 5; ++k) d[k] = fr_[k];
+        d[5] = fr_last_ - fr_entry_;
+        d[6] = fr_entry_;
+    }
+#endif
 }
 
 // lg_ffn_pack: one thread per 16-B fragment of the packed stream (layout: include/lightglue_glue.h)
@@ -1409,18 +1158,18 @@ constexpr int kTileGrid = 256;  // the 256-row forms: one workgroup per CU
 // 32 4.701 -> 4.642, but P = 4 (half a round of 64-row tiles) 1.03-1.04 -> 1.05-1.06 (profiles/r05/
 // ln64_forms_forwards.txt). lg_linear_set_ln_fused: 1 by size (default), 0 always two launches, 2 always one.
 std::atomic<int> g_ln_fused{1};
-// lg_linear_cat_ffn's one-launch form (ffn_kernel) wherever lg_linear_cat_ln_gelu takes its 128-row
-// one-launch form (1) or never (0, the default: its two calls). Measured (profiles/r05/ffn_one_launch_ab.jsonl,
-// ffn_ablations.jsonl): 55.98 vs 52.68 us at P = 16 and forwards 1-3 % slower — phase 2 re-reads W2
-// per 128-row tile (4x the W bytes per row of lg_linear's 256 x 128 tiles: 7.5 us of L2 -> CU traffic),
-// and its epilogue (residual loads, the 16.8 MB store burst, 7.6 us) overlaps nothing with one tile per
-// workgroup, which costs more than h's HBM round trip saves. Kept as an A/B path (lg_linear_set_ffn_fused).
+// lg_linear_cat_ffn's form (lg_linear_set_ffn_fused): 1 (default) the one-launch ffn_rows_kernel when
+// the caller passes the packed weight stream, 0 always its two calls (lg_linear_cat_ln_gelu, then
+// lg_linear with the residual). Measured against the
+// two calls (profiles/r06/ffn_rows_*_ab.jsonl, op alone, us): P = 1 (2,048 rows) 15.5 -> 12.1, P = 4
+// 31.0 -> 14.4, P = 8 32.4 -> 23.4, P = 16 53.6 -> 46.5, P = 32 94.0 -> 87.3; forwards P = 1 / 8 / 16 / 32
+// 0.546 / 1.471 / 2.336 / 4.295 -> 0.501 / 1.204 / 2.145 / 4.029 ms. (Round 5's 128-row one-launch form,
+// ffn_kernel, GELU output in LDS and W2 fragments per 128-row tile from L2: 56 vs 52.7 us at P = 16, not
+// adopted, and removed in round 6: profiles/r05/ffn_one_launch_ab.jsonl.)
 std::atomic<int> g_ffn_fused{1};
-// ffn_rows_kernel's weight-stream depth: k16 steps of fragments in flight per wave (A/B: -DLG_FR_DEPTH)
-#ifndef LG_FR_DEPTH
-#define LG_FR_DEPTH 12
-#endif
-constexpr int kFrDepth = LG_FR_DEPTH;
+// ffn_rows_kernel's weight-stream depth: k16 steps of fragments in flight per wave (measured flat over
+// 6..20 at 2,048 and 8,192 rows: the stream is throughput-bound, profiles/r06/ffn_rows_rowmajor_w_ab.jsonl)
+constexpr int kFrDepth = 12;
 // The tile form (tile_form below): lg_linear_set_wide(0..3) or LG_LINEAR_WIDE forces one (where n
 // allows), for tests and A/B timing; -1 (the default) chooses by size.
 std::atomic<int> g_wide{-2};
@@ -1585,13 +1334,7 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
     p.mtiles = big ? (m + 127) / 128 : (m + 63) / 64;
     p.total = p.mtiles;
     const int grid = p.total < kTileGrid ? p.total : kTileGrid;
-    if (big && LG_LN_2WG) {  // (A/B build: 64-row tiles on 4 waves, two workgroups per CU)
-        p.mtiles = (m + 63) / 64;
-        p.total = p.mtiles;
-        const int g2 = p.total < 2 * kTileGrid ? p.total : 2 * kTileGrid;
-        hipLaunchKernelGGL((linear_ln_kernel<512 / 32, 64, 32, 2, 4>), dim3(g2), dim3(256), 0, stream, p,
-                           (const f16*)gamma, (const f16*)beta, eps);
-    } else if (big)
+    if (big)
         hipLaunchKernelGGL((linear_ln_kernel<512 / 32, 128, 32, 3>), dim3(grid), dim3(512), 0, stream, p,
                            (const f16*)gamma, (const f16*)beta, eps);
     else
@@ -1613,24 +1356,9 @@ int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int
         (w_packed && !aligned16(w_packed)))
         return bad("lg_linear_cat_ffn");
     if (m == 0) return MHA_HD64_STATUS_SUCCESS;
-    const int ffm = g_ffn_fused.load();  // 1 by size (default), 0 two calls, 2 ffn_rows_kernel always, 3 ffn_kernel (A/B)
-    const bool al = k == kLnN && d == kFfnOut && aligned16(b1) && aligned16(gamma) && aligned16(beta) && aligned16(b2) &&
-                    aligned16(out);
-    if (al && w_packed && ((ffm == 1 && m <= kFrMaxRows) || ffm == 2)) {  // few rows: the whole FFN, 32 rows a workgroup
-        LinArgs p{};
-        p.a = (const f16*)x, p.ctx0 = (const f16*)ctx0, p.ctx1 = (const f16*)ctx1, p.w = (const f16*)w1;
-        p.bias = (const f16*)b1, p.out[0] = (f16*)out;
-        p.m = m, p.n = k, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
-        hipLaunchKernelGGL((ffn_rows_kernel<kFrDepth>), dim3((m + kFrMT - 1) / kFrMT), dim3(512), 0, stream, p,
-                           (const f16*)gamma, (const f16*)beta, eps, (const f16*)w_packed, (const f16*)b2);
-        const hipError_t e = hipGetLastError();
-        return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
-                               : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_linear_cat_ffn", hipGetErrorString(e));
-    }
-    const int lnf = g_ln_fused.load();  // as lg_linear_cat_ln_gelu: 1 by size, 2 at every size, 0 never
-    const bool big = m >= 128 * kTileGrid;
-    const bool fused = lnf && ffm == 3 && al && (lnf == 2 || big) && wide_mode() != 0;
-    if (!fused) {  // h in the caller's buffer, then the output projection with the residual
+    const bool one = g_ffn_fused.load() != 0 && w_packed && k == kLnN && d == kFfnOut && aligned16(b1) && aligned16(gamma) &&
+                     aligned16(beta) && aligned16(b2) && aligned16(out);
+    if (!one) {  // h in the caller's buffer, then the output projection with the residual
         const int32_t st = lg_linear_cat_ln_gelu(x, ctx0, ctx1, heads, n0, n1, pairs, w1, b1, gamma, beta, eps, h, stream);
         if (st != MHA_HD64_STATUS_SUCCESS) return st;
         return lg_linear(h, w2, b2, x, m, d, k, out, stream);
@@ -1639,11 +1367,12 @@ int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int
     p.a = (const f16*)x, p.ctx0 = (const f16*)ctx0, p.ctx1 = (const f16*)ctx1, p.w = (const f16*)w1;
     p.bias = (const f16*)b1, p.out[0] = (f16*)out;
     p.m = m, p.n = k, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
-    p.mtiles = (m + 127) / 128;
-    p.total = p.mtiles;
-    const int grid = p.total < kTileGrid ? p.total : kTileGrid;
-    hipLaunchKernelGGL(ffn_kernel, dim3(grid), dim3(512), 0, stream, p, (const f16*)gamma, (const f16*)beta, eps,
-                       (const f16*)w2, (const f16*)b2);
+    if (m <= 32 * kTileGrid)  // one round of 32-row workgroups: the most workgroups (latency)
+        hipLaunchKernelGGL((ffn_rows_kernel<1, kFrDepth>), dim3((m + 31) / 32), dim3(512), 0, stream, p, (const f16*)gamma,
+                           (const f16*)beta, eps, (const f16*)w_packed, (const f16*)b2);
+    else  // several rounds: 64 rows a workgroup, half the weight bytes per row
+        hipLaunchKernelGGL((ffn_rows_kernel<2, kFrDepth>), dim3((m + 63) / 64), dim3(512), 0, stream, p, (const f16*)gamma,
+                           (const f16*)beta, eps, (const f16*)w_packed, (const f16*)b2);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_linear_cat_ffn", hipGetErrorString(e));
@@ -1704,7 +1433,12 @@ int32_t lg_diag_ln_stamps(void* host_dst) {  // (diagnostic build only: not in t
     return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(g_ln_stamps), sizeof(g_ln_stamps)) == hipSuccess ? 0 : 1;
 }
 #endif
+#ifdef LG_FR_STAMPS
+int32_t lg_diag_fr_stamps(void* host_dst) {  // (diagnostic build only: not in the header)
+    return hipMemcpyFromSymbol(host_dst, HIP_SYMBOL(g_fr_stamps), sizeof(g_fr_stamps)) == hipSuccess ? 0 : 1;
+}
+#endif
 int32_t lg_linear_set_ln_fused(int32_t on) { return g_ln_fused.exchange(on == 2 ? 2 : on ? 1 : 0); }
-int32_t lg_linear_set_ffn_fused(int32_t mode) { return g_ffn_fused.exchange(mode < 0 ? 0 : (mode > 3 ? 3 : mode)); }
+int32_t lg_linear_set_ffn_fused(int32_t on) { return g_ffn_fused.exchange(on ? 1 : 0); }
 
 }  // extern "C"

@@ -124,9 +124,8 @@ class _Hip:
     @staticmethod
     def ffn(x, c0, c1, w, b, ln: nn.LayerNorm, w2, b2, packed=None):
         """x + ffn([x | merge_heads(c0, c1)]) (lightglue.py:101-106 with the block's residual):
-        with `packed` (ffn_pack(w, w2)) one launch up to 8,192 rows (ffn_rows_kernel), else
-        linear_cat_ln_gelu into the scratch h, then linear(h, w2, b2, res=x) (include/lightglue_glue.h,
-        lg_linear_set_ffn_fused)."""
+        with `packed` (ffn_pack(w, w2)) one launch (ffn_rows_kernel), else linear_cat_ln_gelu into
+        the scratch h, then linear(h, w2, b2, res=x) (include/lightglue_glue.h, lg_linear_set_ffn_fused)."""
         pr, heads, n0, n1 = c0.shape[0], c0.shape[1], c0.shape[2], c1.shape[2]
         m = pr * (n0 + n1)
         h = torch.empty((1, m, w.shape[0]), dtype=x.dtype, device=x.device)
@@ -440,9 +439,9 @@ class TransformerLayer(nn.Module):
 
     def _forward_fused(self, x, cos, sin, splits, attention: AttnFn):
         """fp16 hip path per block: projection (+rotary/head split), grouped attention, and the FFN
-        with its residual (lg_linear_cat_ffn: one launch up to 8,192 rows, else the input projection
-        gathering [x | heads] with LayerNorm+GELU, then the output projection + residual); the message
-        projection is folded into the FFN's first weight."""
+        with its residual in one launch (lg_linear_cat_ffn with the packed weight stream: the input
+        projection gathering [x | heads], LayerNorm+GELU, the output projection + residual); the
+        message projection is folded into the FFN's first weight."""
         sa, ca = self.self_attn, self.cross_attn
         wq, bq = _qkv_perm(sa, x.dtype)
         qkv = _Hip.linear_qkv_rotary(x, wq, bq, cos, sin, sa.heads, splits)

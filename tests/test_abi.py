@@ -436,9 +436,9 @@ def test_ffn_and_form_hooks_validate_before_touching_the_device(lib):
         assert lib.lg_linear_set_wide(4) == -1
     finally:
         lib.lg_linear_set_wide(prev)
-    prev = lib.lg_linear_set_ffn_fused(7)         # clamped to 3
+    prev = lib.lg_linear_set_ffn_fused(7)         # any nonzero: 1
     try:
-        assert lib.lg_linear_set_ffn_fused(-2) == 3   # clamped to 0
+        assert lib.lg_linear_set_ffn_fused(0) == 1
         assert lib.lg_linear_set_ffn_fused(1) == 0
     finally:
         lib.lg_linear_set_ffn_fused(prev)

@@ -637,18 +637,12 @@ def test_linear_cat_ln_gelu_matches_torch(pairs, n0, n1):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("pairs,n0,n1", [(16, 1024, 1024), (32, 1024, 1024), (17, 1000, 977), (1, 300, 257), (2, 64, 1)])
+@pytest.mark.parametrize("pairs,n0,n1", [(16, 1024, 1024), (17, 1000, 977), (1, 300, 257), (2, 64, 1)])
 def test_linear_cat_ffn_equals_two_calls(pairs, n0, n1):
-    """lg_linear_cat_ffn (the whole FFN with the residual, lightglue.py:101-106 + :150-151) against
-    its two calls (lg_linear_set_ffn_fused(0)): lg_linear_cat_ln_gelu then lg_linear(h, W2, b2, res = x),
-    the default above 8,192 rows (below it, ffn_rows_kernel: test_ffn_rows_kernel). Its 128-row
-    one-launch form (lg_linear_set_ffn_fused(3): ffn_kernel, the GELU output kept in LDS, the second
-    GEMM's W2 fragments from global memory) runs the same operations in the same order, so the outputs
-    are bitwise equal: at lg_linear_cat_ln_gelu's choice (one launch from 32,768 rows: P = 16 / 32;
-    two calls below), the one-launch form forced at
-    every size (lg_linear_set_ln_fused(2): ragged m, a partial last tile, 2 tiles per workgroup at
-    P = 32; below 32,768 rows against the 64-row form of the first half: a few ulps), and the
-    two-call form forced (0)."""
+    """lg_linear_cat_ffn without the packed stream (or with lg_linear_set_ffn_fused(0)) is exactly its
+    two calls: lg_linear_cat_ln_gelu then lg_linear(h, W2, b2, res = x) (lightglue.py:101-106 +
+    :150-151), bitwise, under each of lg_linear_cat_ln_gelu's forms (lg_linear_set_ln_fused 1: by size,
+    2: one launch, 0: two launches)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from lightglue_amd import _lib
@@ -666,36 +660,26 @@ def test_linear_cat_ffn_equals_two_calls(pairs, n0, n1):
         ln = torch.nn.LayerNorm(512).to(dev, dt)
         ln.weight.copy_(1 + 0.1 * rnd(512))
         ln.bias.copy_(0.1 * rnd(512))
+        wp = mt.ffn_pack(w, w2)
         outs = {}
-        hh = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)
-        prev_f = lib.lg_linear_set_ffn_fused(0)
-        default = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2)  # two calls (lg_linear_set_ffn_fused(0))
-        two = mt._Hip.linear(hh, w2, b2, res=x)
-        lib.lg_linear_set_ffn_fused(3)
-        try:
-            for mode in (1, 2, 0):
-                prev = lib.lg_linear_set_ln_fused(mode)
+        for mode in (1, 2, 0):
+            prev = lib.lg_linear_set_ln_fused(mode)
+            try:
+                outs[mode] = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2)           # no packed stream
+                prev_f = lib.lg_linear_set_ffn_fused(0)
                 try:
-                    outs[mode] = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2)
-                    hh = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)
-                    outs[(mode, "two")] = mt._Hip.linear(hh, w2, b2, res=x)
+                    outs[(mode, "off")] = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2, wp)  # one-launch form off
                 finally:
-                    lib.lg_linear_set_ln_fused(prev)
-        finally:
-            lib.lg_linear_set_ffn_fused(prev_f)
+                    lib.lg_linear_set_ffn_fused(prev_f)
+                hh = mt._Hip.linear_cat_ln_gelu(x, c0, c1, w, b, ln)
+                outs[(mode, "two")] = mt._Hip.linear(hh, w2, b2, res=x)
+            finally:
+                lib.lg_linear_set_ln_fused(prev)
         torch.cuda.synchronize()
-    assert torch.equal(default, two)
-    big = pairs * (n0 + n1) >= 256 * 128
     for mode in (1, 2, 0):
         assert torch.isfinite(outs[mode]).all(), mode
-        d = float((outs[mode].float() - outs[(mode, "two")].float()).abs().max())
-        if mode == 2 and not big:
-            # (forced below 32,768 rows, lg_linear_cat_ln_gelu takes its 64-row tiles, whose row
-            # statistics sum 8 partials where the 128-row tiles of ffn_kernel sum 4: h can differ
-            # by an ulp, the output by a few)
-            assert d <= 4e-3, (mode, d)
-        else:
-            assert torch.equal(outs[mode], outs[(mode, "two")]), (mode, d)
+        assert torch.equal(outs[mode], outs[(mode, "two")]), mode
+        assert torch.equal(outs[(mode, "off")], outs[(mode, "two")]), mode
 
 
 def _ffn_torch(x, c0, c1, w, b, ln, w2, b2):
@@ -721,13 +705,14 @@ def _ulp_bound(out, x, k=2.0):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("pairs,n0,n1", [(1, 512, 512), (1, 1024, 1024), (1, 2048, 2048), (1, 700, 1301), (1, 1, 63),
-                                         (3, 37, 70), (4, 1024, 1024), (5, 1000, 1011), (1, 3, 2)])
+                                         (3, 37, 70), (4, 1024, 1024), (5, 1000, 1011), (1, 3, 2), (8, 1024, 1024),
+                                         (9, 1000, 1011)])
 def test_ffn_rows_kernel(pairs, n0, n1):
-    """lg_linear_cat_ffn's one-launch form for few rows (ffn_rows_kernel, 32 rows per workgroup, the
-    default up to 8,192 rows; lg_linear_set_ffn_fused(2) forces it) against its two calls (0) and the
-    torch restatement of the fp16 model (_ffn_torch): single pairs of 512 / 1024 / 2048 keypoints,
-    ragged rows (a partial last workgroup, images of 1..3 rows), 4 pairs (8,192 rows: the last size the
-    default takes it) and 5 pairs forced (past it)."""
+    """lg_linear_cat_ffn's one-launch form (ffn_rows_kernel: 32 rows per workgroup up to one round of
+    them, 8,192 rows; 64 rows beyond; the default) against its two calls (lg_linear_set_ffn_fused(0))
+    and the torch restatement of the fp16 model (_ffn_torch): single pairs of 512 / 1024 / 2048
+    keypoints, ragged rows (a partial last workgroup, images of 1..3 rows), 4 pairs (8,192 rows: the
+    last 32-row size), 5 pairs (64-row tiles, a partial last one), 8 and 9 pairs (2 / 3 rounds)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from lightglue_amd import _lib
@@ -750,16 +735,17 @@ def test_ffn_rows_kernel(pairs, n0, n1):
         packed_c = torch.empty(lib.lg_ffn_packed_bytes(h) // 2, dtype=dt, device=dev)
         assert lib.lg_ffn_pack(w.data_ptr(), w2.data_ptr(), h, packed_c.data_ptr(), None) == 0
         outs = {}
-        for mode in (0, 2, 1):
+        for mode in (0, 1):
             prev = lib.lg_linear_set_ffn_fused(mode)
             try:
                 outs[mode] = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2, wp)
             finally:
                 lib.lg_linear_set_ffn_fused(prev)
+        outs[2] = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2, wp)     # the default
         no_pack = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2)  # (without the packed stream: the two calls)
         ref = _ffn_torch(x, c0, c1, w, b, ln, w2, b2)
         torch.cuda.synchronize()
-    two, rows = outs[0].float(), outs[2].float()
+    two, rows = outs[0].float(), outs[1].float()
     assert torch.isfinite(rows).all()
     d = (rows - two).abs()
     err_rows, err_two = float((rows - ref.float()).abs().max()), float((two - ref.float()).abs().max())
@@ -767,7 +753,7 @@ def test_ffn_rows_kernel(pairs, n0, n1):
           f"differ), vs torch: rows {err_rows:.3e}, two calls {err_two:.3e}")
     assert bool((d <= _ulp_bound(two, x)).all()), float(d.max())
     assert err_rows <= 2e-2 and err_two <= 2e-2
-    assert torch.equal(outs[1], outs[2] if m <= 8192 else outs[0])  # the default's choice by size
+    assert torch.equal(outs[2], outs[1])  # the default: one launch
     assert torch.equal(no_pack, outs[0]) and torch.equal(packed_c, wp)  # lg_ffn_pack == ffn_pack
 
 

@@ -1,5 +1,5 @@
-"""A/B timing of lg_linear_cat_ffn's forms (lg_linear_set_ffn_fused: 0 its two calls, 1 by size, 2 the
-32-row one-launch ffn_rows_kernel at every size, 3 the 128-row ffn_kernel) — the op alone at P pairs of
+"""A/B timing of lg_linear_cat_ffn's forms (lg_linear_set_ffn_fused: 0 its two calls, 1 the one-launch
+ffn_rows_kernel) — the op alone at P pairs of
 n keypoints (a graph of back-to-back calls per form, replays interleaved), then whole fp16 matcher
 forwards (graph replay, interleaved), with the max |difference| of each form's outputs from the first.
 
@@ -39,7 +39,7 @@ def sizes(s):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--modes", default="0,2")
+    ap.add_argument("--modes", default="0,1")
     ap.add_argument("--ops", default="1x512,1x1024,1x2048,2x1024,4x1024,8x1024")
     ap.add_argument("--forwards", default="1x512,1x1024,1x2048,4x1024")
     ap.add_argument("--reps", type=int, default=20)

@@ -1,0 +1,59 @@
+"""Diagnostic: where ffn_rows_kernel's time goes (stamps build, -DLG_FR_STAMPS: per wave, s_memtime
+cycles of chained segments; see csrc/lightglue_linear.hip).
+
+    MHA_HD64_LIB=lib/ab/libmha_hd64_frstamps.so python tools/fr_stamps.py [P=1] [n=1024]
+"""
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "lightglue-with-flashattentionv2-tensorrt_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from lightglue_amd import _lib  # noqa: E402
+from lightglue_amd import matcher as mt  # noqa: E402
+
+
+def main():
+    P = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    lib = _lib.load()
+    fn = lib.lg_diag_fr_stamps
+    fn.restype, fn.argtypes = ctypes.c_int32, [ctypes.c_void_p]
+    dev, dt, h = torch.device("cuda:0"), torch.float16, 4
+    M = P * 2 * n
+    g = torch.Generator().manual_seed(3)
+    rnd = lambda *s: torch.randn(*s, generator=g).to(dev, dt)  # noqa: E731
+    x = rnd(1, M, 256) * 0.5
+    c0, c1 = rnd(P, h, n, 64), rnd(P, h, n, 64)
+    w, b, w2, b2 = rnd(512, 512) * 0.05, rnd(512) * 0.1, rnd(256, 512) * 0.05, rnd(256) * 0.1
+    ln = torch.nn.LayerNorm(512).to(dev, dt)
+    wp = mt.ffn_pack(w, w2)
+    names = ["prologue", "phase1", "layernorm_gelu", "phase2", "epilogue", "total"]
+    wgs = min(256, (M + 31) // 32 if M <= 8192 else (M + 63) // 64)  # (stamps of the first 256)
+    rows = []
+    for rep in range(6):
+        for _ in range(3):  # back to back, as in a forward
+            mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2, wp)
+        torch.cuda.synchronize()
+        buf = np.zeros(256 * 8 * 8, dtype=np.uint64)
+        assert fn(buf.ctypes.data) == 0
+        a = buf.reshape(256, 8, 8)[:wgs].astype(np.int64)
+        if rep:
+            rows.append(a)
+    a = np.concatenate(rows, 0)
+    out = {"P": P, "n": n, "M": M, "workgroups": wgs,
+           "median_cycles": {k: float(np.median(a[:, :, i])) for i, k in enumerate(names)},
+           "max_total": float(a[:, :, 5].max()),
+           "entry_spread_cycles": float(np.median(a[:, :, 6].max(1) - a[:, :, 6].min(1)))}
+    last = rows[-1]
+    ent = last[:, :, 6]
+    out["launch_entry_spread_cycles"] = float(ent.max() - ent.min())
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

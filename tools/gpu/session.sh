@@ -3,6 +3,7 @@
 # failure (no GPU step runs after a fault, abort or timeout). Logs in gpurun_out/<tag>/.
 #   bash tools/gpu/session.sh <tag> <step> [<step> ...]
 # steps: tests[:<pytest -k expr>]  gpu  ffn_ab[:<args>]  bench[:<args>]  smoke  prof_fwd:<P>x<n>
+#        pmc_ffn:<P>:<n>:<mode>
 set -o pipefail
 tag=$1; shift
 O=$PWD/gpurun_out/$tag; mkdir -p "$O"
@@ -30,6 +31,15 @@ for step in "$@"; do
                 -d "$O/fwd_${P}x${n}" -o m -- python3 "$R/tools/matcher_profile.py" "$P" "$n" 10) || exit $?
             f=$(find "$O/fwd_${P}x${n}" -name "m_kernel_trace.csv" | head -1)
             python3 tools/forward_timeline.py "$f" > "$O/timeline_${P}x${n}.txt" 2>&1; cat "$O/timeline_${P}x${n}.txt" | head -20 ;;
+        pmc_ffn)  # counter passes over lg_linear_cat_ffn at P x n (arg P:n:mode)
+            IFS=: read -r P n mode <<< "$arg"; R=$PWD
+            for pass in "A:SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA" \
+                        "B:SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" \
+                        "C:FETCH_SIZE" "D:WRITE_SIZE" "E:SQ_INSTS_SALU SQ_INSTS_VMEM SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE"; do
+                pn=${pass%%:*}; ctr=${pass#*:}
+                (cd /tmp && TMPDIR=/tmp run 120 "pmc_ffn_${P}_${mode}_$pn.log" rocprofv3 --pmc $ctr --output-format csv \
+                    -d "$O/pmc_ffn_${P}_${mode}_$pn" -o p -- python3 "$R/tools/ffn_driver.py" "$P" "$n" "$mode" 20) || exit $?
+            done ;;
         *) echo "unknown step $name"; exit 2 ;;
     esac
 done
