@@ -142,6 +142,18 @@ int32_t lg_log_double_softmax_f16(const void* sim, const void* z0, const void* z
                                   int64_t z_row_stride, int32_t m, int32_t n, int32_t batch, float* scores,
                                   void* workspace, hipStream_t stream);
 
+/* The fp16 assignment head in two launches (round 6): v [batch][m + n][ld] fp16 is the final
+ * projection of both images' rows (image 0's m rows, then image 1's n; pairs pair_stride elements
+ * apart), channels 0..255 the scaled descriptors m0 / m1 (final_proj(d) / d^0.25) and channel zc
+ * (>= 256) the matchability logit. scores [batch, m, n] fp32 = log_softmax(sim, 2) + log_softmax(sim, 1)
+ * + logsig(z0) + logsig(z1)ᵀ with sim = m0 · m1ᵀ rounded to fp16 (lightglue.py:208-233): the similarity
+ * by MFMA and each row's and column's exact logsumexp in one launch (a workgroup owns 32 rows of one
+ * image against all of the other), the combine in a second. m, n <= 2048, n % 8 == 0, ld % 8 == 0;
+ * v, scores, workspace 16-B aligned; workspace >= lg_assign_scores_workspace(m, n, batch) bytes. */
+size_t lg_assign_scores_workspace(int32_t m, int32_t n, int32_t batch);
+int32_t lg_assign_scores(const void* v, int64_t pair_stride, int32_t ld, int32_t zc, int32_t m, int32_t n, int32_t batch,
+                         float* scores, void* workspace, hipStream_t stream);
+
 /* The fp16 forward's inputs (lightglue.py:329-337 and FourierPositionalEncoding :32-52), round 5:
  * x [pairs * (n0 + n1), dim] pair-major from desc0 [pairs, n0, dim] and desc1 [pairs, n1, dim]
  * (dim = 256, 16-B aligned), and the rotary tables cos, sin [pairs * (n0 + n1), 64] from kpts0
@@ -153,12 +165,11 @@ int32_t lg_pair_inputs(const void* desc0, const void* desc1, const void* kpts0, 
 
 /* Test and benchmark hook: the projections' tile forms for launches of many rows (several image
  * pairs per forward): 0 the 64 x 64 form only, 1 the 256 x 128 form where n allows, 2 the
- * 256 x 256 form where n allows (plain bias outputs; else 1), 3 the 128 x 256 form (A/B only),
- * 4 the 128 x 128 form on 4 waves (two workgroups per CU; the by-size choice from 128 of its
- * tiles and 8,192 rows on), 5 the same with 32-deep K steps (A/B only), -1 (the default) chosen by size; values
- * outside -1..5 are clamped. The environment variable
- * LG_LINEAR_WIDE sets the initial mode the same way. Every form gives the same bits. Returns the
- * previous mode. */
+ * 256 x 256 form where n allows (plain bias outputs; else 1), 4 the 128 x 128 form on 4 waves (two
+ * workgroups per CU; the by-size choice from 128 of its tiles and 8,192 rows on), -1 (the default)
+ * chosen by size; 3 and 5 (round 5's A/B forms, removed) select 1 and 4; values outside -1..5 are
+ * clamped. The environment variable LG_LINEAR_WIDE sets the initial mode the same way. Every form
+ * gives the same bits. Returns the previous mode. */
 int32_t lg_linear_set_wide(int32_t mode);
 
 /* Test and benchmark hook for lg_linear_cat_ln_gelu's forms: 1 (the default) one launch from a full

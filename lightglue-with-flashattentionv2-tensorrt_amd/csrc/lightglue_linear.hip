@@ -30,6 +30,7 @@
 #include "lightglue_glue.h"
 #include "mha_hd64.h"
 #include "mha_hd64_internal.h"
+#include "mha_hd64_device.h"  // (lds_dma16: the inline-asm LDS-DMA piece)
 
 namespace {
 
@@ -350,7 +351,7 @@ __device__ __forceinline__ void tile_issue(const TileSrc<NWP, NAP>& t, int ks, c
 }
 
 // ---- the 256-row forms, for launches with many rows (several image pairs per forward) ----
-// Persistent tiles of MT rows x NT channels (256 x 128, 256 x 256 or 128 x 256), 8 waves as WM (m) x
+// Persistent tiles of MT rows x NT channels (256 x 128 or 256 x 256 on 8 waves, 128 x 128 on 4), NWV waves as WM (m) x
 // WN (n) tiles of 64 rows x NT / WN channels (2 x NB MFMA blocks of 32 x 32), K in BK-deep steps through
 // an NST-stage LDS-DMA ring (16-B units XOR-swizzled on the source address: conflict-free
 // ds_read_b128), NST - 1 steps in flight; the ring runs on across tile seams, so the next tile's
@@ -1146,6 +1147,221 @@ __global__ __launch_bounds__(256) void ffn_pack_kernel(const f16* __restrict__ w
     *reinterpret_cast<f16x8*>(packed + (size_t)f * 8) = *reinterpret_cast<const f16x8*>(src);
 }
 
+// ---- the assignment head: similarity + dual log-softmax in two launches (lg_assign_scores, round 6) ----
+// MatchAssignment (lightglue.py:208-233) on the fp16 model: sim = m0 · m1ᵀ (fp16 out, the reference's
+// bmm), scores = log_softmax(sim, 2) + log_softmax(sim, 1) + logsig(z0) + logsig(z1)ᵀ. Round 5 ran the
+// similarity as a framework GEMM and three glue launches (row pass, column pass, combine: ~31 us per
+// single-pair forward at n = 1,024, profiles/r05/single_pair_timelines.txt). Here:
+//  * assign_lse_kernel: a workgroup owns 32 rows of ONE image and computes their similarity against
+//    1/S of the OTHER image's rows by MFMA (own rows in LDS, the other image streamed per wave through
+//    a 2-slot LDS-DMA ring of 128-deep K halves, whole 256-B row pieces), then the (max, sum of
+//    exponentials) of each own row over that share, reduced over the 8 waves through LDS. Image-0
+//    workgroups give the row partials (and write sim in fp16 for the combine), image-1 workgroups the
+//    column partials: no cross-workgroup exchange. (An image-1 workgroup recomputes its columns of sim
+//    with the operands swapped: the same products in the same k-step order.) S splits of the other
+//    image fill the chip at a single pair (each workgroup then streams 1/S of it).
+//  * assign_combine_kernel: closes the S partials of each row and column (fixed order) into the
+//    logsumexps and writes scores = 2 sim + (logsig(z0) - lse_row) + (logsig(z1) - lse_col), fp32.
+struct AsArgs {
+    const f16* v;     // [batch][m + n][ld]: image 0's rows then image 1's; channels 0..255 the scaled
+                      // final projection, channel zc the matchability logit
+    long ps;          // pair stride of v (elements)
+    int ld, zc, m, n, rb0, S;
+    f16* sim;         // workspace [batch][m][n]
+    float2* rpart;    // workspace [batch][S][m]: (max, sum of exp) of row i over split s
+    float2* cpart;    // workspace [batch][S][n]: the same for column j
+    float* scores;    // [batch][m][n]
+};
+__device__ __forceinline__ float log_sigmoid_f(float z) { return fminf(z, 0.f) - log1pf(__expf(-fabsf(z))); }
+
+template <int BPW>  // 32-row blocks of the other image per wave
+__global__ __launch_bounds__(512, 1) void assign_lse_kernel(AsArgs a) {
+    constexpr int kOwn = 0;                       // own rows [32][512 B], units XOR (row & 15)
+    constexpr int kRing = 32 * 512;               // per wave 2 slots of [32][256 B]
+    constexpr int kRed = kRing + 8 * 2 * 8192;    // [32 rows][8 waves] fp32
+    __shared__ __attribute__((aligned(16))) char smem[kRed + 32 * 8 * 4];
+    lds_char* const lds = (lds_char*)smem;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, hh = lane >> 5;
+    const int p = blockIdx.y, sp = blockIdx.z;
+    const bool side = (int)blockIdx.x >= a.rb0;
+    const int o0 = (side ? (int)blockIdx.x - a.rb0 : (int)blockIdx.x) * 32;
+    const int nown = side ? a.n : a.m, noth = side ? a.m : a.n;
+    const f16* const vp = a.v + (size_t)p * a.ps;
+    const f16* const own = vp + (size_t)(side ? a.m : 0) * a.ld;
+    const f16* const oth = vp + (size_t)(side ? 0 : a.m) * a.ld;
+
+    // own rows: 32 rows x 32 units, two per thread
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int u = i * 512 + tid, row = u >> 5, un = u & 31;
+        const f16x8 x = *reinterpret_cast<const f16x8*>(own + (size_t)min(o0 + row, nown - 1) * a.ld + un * 8);
+        *(lds_f16x8*)(lds + kOwn + row * 512 + ((un ^ (row & 15)) << 4)) = x;
+    }
+    // the other image's rows, streamed per wave: block t of this wave = other rows 32 ((t S + sp) 8 + w);
+    // chunk c = (block t, K half hk) -> slot c & 1
+    const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(oth), (short)0,
+                                                                         (int)((size_t)noth * a.ld * 2), 0x00020000);
+    auto blk_row0 = [&](int t) { return ((t * a.S + sp) * 8 + wave) * 32; };
+    auto issue = [&](int c) {  // 8 pieces of 4 rows x 256 B; lane -> (row 4 i + lane / 16, unit lane % 16)
+        const int t = c >> 1, hk = c & 1;
+        const unsigned m0 = mha_hd64::lds_addr(smem + kRing + wave * 16384 + (c & 1) * 8192);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int row = 4 * i + (lane >> 4), pu = lane & 15;
+            const int grow = min(blk_row0(t) + row, noth - 1);
+            const unsigned voff = (unsigned)(grow * a.ld * 2 + hk * 256 + ((pu ^ (row & 15)) << 4));
+            mha_hd64::lds_dma16(m0 + i * 1024, voff, ors, 0);
+        }
+    };
+    constexpr int nch = 2 * BPW;
+    auto live = [&](int t) { return blk_row0(t) < noth; };  // (wave-uniform)
+    if (live(0)) issue(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // own rows in LDS
+
+    f16 sv[BPW][16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < BPW; ++t) {
+        f32x16 acc = {};
+        if (live(t)) {
+#pragma unroll
+            for (int hk = 0; hk < 2; ++hk) {
+                const int c = 2 * t + hk;
+                // the next chunk in flight, then this one landed (this wave's own pieces: no barrier)
+                if (c + 1 < nch && live((c + 1) >> 1)) {
+                    issue(c + 1);
+                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                const unsigned sb = kRing + wave * 16384 + (c & 1) * 8192;
+#pragma unroll
+                for (int s = 0; s < 8; ++s) {
+                    const int u = 2 * s + hh;
+                    const f16x8 af = *(lds_f16x8*)(lds + sb + r * 256 + ((u ^ (r & 15)) << 4));
+                    const int uo = 16 * hk + u;
+                    const f16x8 bf = *(lds_f16x8*)(lds + kOwn + r * 512 + ((uo ^ (r & 15)) << 4));
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(af, bf, acc, 0, 0, 0);
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the slot is refilled next chunk)
+            }
+        }
+        // lane (r, hh): acc[4 g + e] = sim of own row o0 + r with other row blk_row0(t) + 8 g + 4 hh + e
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int j0 = blk_row0(t) + 8 * g + 4 * hh;
+            f16x4 h4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const f16 h = (f16)acc[4 * g + e];
+                h4[e] = h;
+                sv[t][4 * g + e] = (j0 + e < noth) ? h : (f16)-INFINITY;
+                mx = fmaxf(mx, (float)sv[t][4 * g + e]);
+            }
+            if (!side && o0 + r < a.m && j0 < a.n)
+                *reinterpret_cast<f16x4*>(a.sim + ((size_t)p * a.m + o0 + r) * a.n + j0) = h4;
+        }
+    }
+    // (max, sum of exp) of each own row over this split: the max over the 8 waves, then the sum
+    float* const red = (float*)(void*)(smem + kRed);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (hh == 0) red[r * 8 + wave] = mx;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    float M = red[r * 8];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) M = fmaxf(M, red[r * 8 + w]);
+    float s = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+        for (int t = 0; t < BPW; ++t)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) s += __expf((float)sv[t][e] - M);
+    }
+    s += __shfl_xor(s, 32, 64);
+    __builtin_amdgcn_s_barrier();  // (every wave has read the maxima)
+    if (hh == 0) red[r * 8 + wave] = s;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wave == 0 && hh == 0 && o0 + r < nown) {
+        float tot = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) tot += red[r * 8 + w];
+        (side ? a.cpart + ((size_t)p * a.S + sp) * a.n : a.rpart + ((size_t)p * a.S + sp) * a.m)[o0 + r] = make_float2(M, tot);
+    }
+}
+
+// the logsumexp of S (max, sum) partials, merged in split order
+__device__ __forceinline__ float lse_close(const float2* part, size_t stride, int S) {
+    float mx = -INFINITY, s = 0.f;
+    for (int k = 0; k < S; ++k) {
+        const float2 q = part[k * stride];
+        if (q.x == -INFINITY) continue;
+        if (q.x > mx) {
+            s = s * __expf(mx - q.x) + q.y;
+            mx = q.x;
+        } else {
+            s += q.y * __expf(q.x - mx);
+        }
+    }
+    return mx + __logf(s);
+}
+
+// scores = 2 sim + (logsig(z0[i]) - lse_row[i]) + (logsig(z1[j]) - lse_col[j]) (fp32), W waves per
+// block, 8 rows per wave, 16-B loads / stores
+template <int CPL, int W>  // columns per lane in units of 8 (n <= 512 CPL)
+__global__ __launch_bounds__(64 * W) void assign_combine_kernel(AsArgs a) {
+    const int p = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const f16* const vp = a.v + (size_t)p * a.ps;
+    __shared__ float ct[512 * CPL];
+    for (int j = threadIdx.x; j < a.n; j += 64 * W)
+        ct[j] = log_sigmoid_f((float)vp[(size_t)(a.m + j) * a.ld + a.zc]) -
+                lse_close(a.cpart + (size_t)p * a.S * a.n + j, a.n, a.S);
+    __syncthreads();
+    const int i0 = (blockIdx.x * W + wave) * 8;
+    if (i0 >= a.m) return;
+    const int i1 = min(i0 + 8, a.m);
+    const f16* sim = a.sim + (size_t)p * a.m * a.n;
+    float* out = a.scores + (size_t)p * a.m * a.n;
+    f16x8 x[8][CPL];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const int i = min(i0 + b, i1 - 1);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int j = (c * 64 + lane) * 8;
+            if (j < a.n) x[b][c] = *reinterpret_cast<const f16x8*>(sim + (size_t)i * a.n + j);
+        }
+    }
+    float rt[8];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const int i = min(i0 + b, i1 - 1);
+        rt[b] = log_sigmoid_f((float)vp[(size_t)i * a.ld + a.zc]) - lse_close(a.rpart + (size_t)p * a.S * a.m + i, a.m, a.S);
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        if (i0 + b >= i1) break;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int j = (c * 64 + lane) * 8;
+            if (j >= a.n) continue;
+            f32x4 o0, o1;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                o0[e] = 2.f * (float)x[b][c][e] + rt[b] + ct[j + e];
+                o1[e] = 2.f * (float)x[b][c][e + 4] + rt[b] + ct[j + e + 4];
+            }
+            *reinterpret_cast<f32x4*>(out + (size_t)(i0 + b) * a.n + j) = o0;
+            *reinterpret_cast<f32x4*>(out + (size_t)(i0 + b) * a.n + j + 4) = o1;
+        }
+    }
+}
+
 constexpr int kTileGrid = 256;  // the 256-row forms: one workgroup per CU
 // lg_linear_cat_ln_gelu's one-launch form (linear_ln_kernel), by size: its 128-row tiles from one
 // full round of them on (256: M >= 32,768 rows, P >= 16 pairs of 1024 keypoints), its 64-row tiles
@@ -1194,15 +1410,16 @@ bool aligned8(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 7) == 0;
 
 // The 256-row tile forms (linear_tile_kernel): 1 = 256 x 128, 2 = 256 x 256 (32-deep K steps, 4
 // stages; plain EPI_BIAS only: the residual / rotary tables and the scatter addressing do not fit
-// beside its accumulators), 3 = 128 x 256; 4 / 5 = 128 x 128 on 4 waves, two workgroups per CU
-// (64-deep K steps through 2 stages / 32-deep through 4). Form 4 against form 1 (profiles/r05/
+// beside its accumulators), 4 = 128 x 128 on 4 waves, two workgroups per CU (64-deep K steps through
+// 2 stages). (Round 5's A/B forms 3 = 128 x 256 and 5 = form 4 with 32-deep K steps through 4 stages,
+// both slower, were removed in round 6; 3 and 5 now select 1 and 4.) Form 4 against form 1 (profiles/r05/
 // tile_form4_ab.jsonl, us): qkv 18.5 / 26.6 / 48.8 -> 15.9 / 25.1 / 46.5 at P = 8 / 16 / 32, split2
 // 17.5 -> 17.0 and linear+res 12.2 / 16.9 / 30.7 -> 9.8 / 16.6 / 28.5 (form 1 leaves half the CUs idle
 // at P = 8), cat 14.5 / 24.6 / 45.1 -> 14.8 / 24.3 / 46.0; at P = 4 qkv 10.9 = 10.9, split2 8.6 -> 7.4,
 // linear+res 10.5 (64 x 64) -> 8.1, cat 11.5 -> 9.3; whole forwards P = 4 / 8 / 16 +2.3 / +2.9 / +0.8 %,
-// P = 32 -1.0 % (form_fwd_ab.jsonl): the default below; forms 1-3 (the round's earlier default was form 1
-// from half a round of its tiles) stay for lg_linear_set_wide / LG_LINEAR_WIDE, which force a form where
-// n and the operand alignment allow.
+// P = 32 -1.0 % (form_fwd_ab.jsonl): the default below; forms 1 and 2 (the round's earlier default was
+// form 1 from half a round of its tiles) stay for lg_linear_set_wide / LG_LINEAR_WIDE, which force a
+// form where n and the operand alignment allow.
 int tile_form(const LinArgs& p, int epi, bool gather) {
     bool al = aligned16(p.bias);
     const int nout = epi == EPI_BIAS ? 1 : epi == EPI_QKV_ROTARY ? 6 : 4;
@@ -1222,11 +1439,9 @@ int tile_form(const LinArgs& p, int epi, bool gather) {
     // with the 64 x 64 form everywhere, P = 4 / 8 / 16 7 / 3 / 1 % faster than form 1 with this rule)
     (void)gather;
     const int f = w >= 0 ? w : (p.m >= 8192 && (long)((p.m + 127) / 128) * (p.n / 128) >= 128 ? 4 : 0);
-    if (f == 1 && p.n % 128 == 0) return 1;
     if (f == 2 && p.n % 256 == 0) return (p.res || epi != EPI_BIAS) ? 1 : 2;
-    if (f == 3 && p.n % 256 == 0) return 3;
-    if (f >= 4 && p.n % 128 == 0) return f;
-    return f >= 1 && p.n % 128 == 0 ? 1 : 0;
+    if (f >= 4 && p.n % 128 == 0) return 4;  // (5: round 5's 32-deep A/B variant of form 4, removed in round 6)
+    return f >= 1 && p.n % 128 == 0 ? 1 : 0;  // (3: round 5's 128 x 256 A/B form, removed in round 6)
 }
 
 template <int EPI, bool GATHER, bool RES, int MT, int NT, int BK, int NST, int NWV>
@@ -1258,9 +1473,7 @@ int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
         case 2:
             if constexpr (!GATHER && EPI == EPI_BIAS) launch_tile<EPI, GATHER, 256, 256, 32, 4>(p, stream);
             break;
-        case 3: launch_tile<EPI, GATHER, 128, 256, 64, 3>(p, stream); break;
         case 4: launch_tile<EPI, GATHER, 128, 128, 64, 2, 4>(p, stream); break;
-        case 5: launch_tile<EPI, GATHER, 128, 128, 32, 4, 4>(p, stream); break;
         default:
             p.mtiles = (p.m + kBM - 1) / kBM;
             p.total = p.mtiles * (p.n / kBN);
@@ -1387,6 +1600,66 @@ int32_t lg_ffn_pack(const void* w1, const void* w2, int32_t heads, void* packed,
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_ffn_pack", hipGetErrorString(e));
+}
+
+namespace {
+// lg_assign_scores' split of the other image: enough workgroups for one round of the chip (256)
+int assign_splits(int32_t m, int32_t n, int32_t batch) {
+    const long base = (long)((m + 31) / 32 + (n + 31) / 32) * batch;
+    int S = 1;
+    while (S < 8 && base * S * 2 <= 256) S *= 2;
+    return S;
+}
+}  // namespace
+
+size_t lg_assign_scores_workspace(int32_t m, int32_t n, int32_t batch) {
+    if (m <= 0 || n <= 0 || batch <= 0) return 0;
+    const size_t b = (size_t)batch, S = (size_t)assign_splits(m, n, batch);
+    return (b * m * n * 2 + 255) / 256 * 256 + (b * S * m * 8 + 255) / 256 * 256 + (b * S * n * 8 + 255) / 256 * 256;
+}
+
+int32_t lg_assign_scores(const void* v, int64_t pair_stride, int32_t ld, int32_t zc, int32_t m, int32_t n, int32_t batch,
+                         float* scores, void* workspace, hipStream_t stream) {
+    if (m < 0 || n < 0 || batch < 0 || m > 2048 || n > 2048 || n % 8 != 0 || ld < 256 || ld % 8 != 0 || zc < 256 ||
+        zc >= ld || pair_stride < (int64_t)(m + n) * ld ||
+        ((m > 0 && n > 0 && batch > 0) && (!v || !scores || !workspace || !aligned16(v) || !aligned16(scores) ||
+                                          !aligned16(workspace))))
+        return bad("lg_assign_scores");
+    if (m == 0 || n == 0 || batch == 0) return MHA_HD64_STATUS_SUCCESS;
+    AsArgs a{};
+    a.v = (const f16*)v, a.ps = (long)pair_stride, a.ld = ld, a.zc = zc, a.m = m, a.n = n, a.rb0 = (m + 31) / 32;
+    a.S = assign_splits(m, n, batch);
+    char* ws = (char*)workspace;
+    const size_t b = (size_t)batch, S = (size_t)a.S;
+    a.sim = (f16*)ws;
+    a.rpart = (float2*)(ws + (b * m * n * 2 + 255) / 256 * 256);
+    a.cpart = (float2*)((char*)a.rpart + (b * S * m * 8 + 255) / 256 * 256);
+    a.scores = scores;
+    const dim3 g1(a.rb0 + (n + 31) / 32, batch, a.S);
+    const int oth = m > n ? m : n;  // other-image blocks per wave: ceil(blocks / (8 S))
+    const int bpw = ((oth + 31) / 32 + 8 * a.S - 1) / (8 * a.S);
+    if (bpw <= 1) hipLaunchKernelGGL(assign_lse_kernel<1>, g1, dim3(512), 0, stream, a);
+    else if (bpw <= 2) hipLaunchKernelGGL(assign_lse_kernel<2>, g1, dim3(512), 0, stream, a);
+    else if (bpw <= 4) hipLaunchKernelGGL(assign_lse_kernel<4>, g1, dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL(assign_lse_kernel<8>, g1, dim3(512), 0, stream, a);
+    // combine: 8 rows per wave; 8-wave blocks where they fill the chip, else one wave per block
+    const bool small = (long)((m + 63) / 64) * batch < 256;
+    const int W = small ? 1 : 8;
+    const dim3 g2((m + 8 * W - 1) / (8 * W), batch);
+#define LG_AC(CPL)                                                                                          \
+    if (small) hipLaunchKernelGGL((assign_combine_kernel<CPL, 1>), g2, dim3(64), 0, stream, a);             \
+    else hipLaunchKernelGGL((assign_combine_kernel<CPL, 8>), g2, dim3(512), 0, stream, a);
+    if (n <= 512) {
+        LG_AC(1)
+    } else if (n <= 1024) {
+        LG_AC(2)
+    } else {
+        LG_AC(4)
+    }
+#undef LG_AC
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
+                           : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_assign_scores", hipGetErrorString(e));
 }
 
 int32_t lg_linear_qkv_rotary(const void* x, const void* w_perm, const void* b_perm, const void* cosv,

@@ -218,6 +218,23 @@ class _Hip:
         _check(st, "lg_log_double_softmax_f16")
         return out
 
+    _last_assign_ws = None  # (tests read the similarity copy the kernel leaves in its workspace)
+
+    @staticmethod
+    def assign_scores(v, m, zc):
+        """v [P, m + n, C] fp16: the assignment projection of both images' rows (scaled descriptors at
+        channels 0..255, the matchability logit at zc) -> fp32 scores [P, m, n] (lg_assign_scores: the
+        similarity and the dual log-softmax in two launches)."""
+        pr, n, ch = v.shape[0], v.shape[1] - m, v.shape[2]
+        lib = _lib.load()
+        out = torch.empty((pr, m, n), dtype=torch.float32, device=v.device)
+        stream = _Hip._stream(v)
+        ws = _workspace(v.device, stream, lib.lg_assign_scores_workspace(m, n, pr))
+        _Hip._last_assign_ws = ws
+        st = lib.lg_assign_scores(v.data_ptr(), (m + n) * ch, ch, zc, m, n, pr, out.data_ptr(), ws.data_ptr(), stream)
+        _check(st, "lg_assign_scores")
+        return out
+
     @staticmethod
     def pair_inputs(desc0, desc1, kpts0, kpts1, wr):
         """x [1, P*(m+n), 256] pair-major and the rotary tables cos, sin [1, P*(m+n), 64] in one launch."""
@@ -473,14 +490,14 @@ class MatchAssignment(nn.Module):
         self.final_proj = nn.Linear(d, d)
         self.matchability = nn.Linear(d, 1)
 
-    def hip16_ok(self, x: torch.Tensor, n: int) -> bool:
-        return x.dtype == torch.float16 and x.is_cuda and x.shape[-1] == 256 and n % 8 == 0 and n <= 2048
+    def hip16_ok(self, x: torch.Tensor, m: int, n: int) -> bool:
+        return x.dtype == torch.float16 and x.is_cuda and x.shape[-1] == 256 and n % 8 == 0 and n <= 2048 and m <= 2048
 
     def forward_rows(self, x: torch.Tensor, pr: int, m: int, n: int) -> torch.Tensor:
         """fp16 hip path on both images' rows x [1, P*(m+n), d] at once: ONE projection with
-        [W_final / scale ; w_match ; 0], the similarity as one batched GEMM on the fp16 halves, and
-        the dual log-softmax reading the fp16 similarity and the matchability channel directly
-        (lightglue.py:208-233). d^0.25 = 4 for d = 256, a power of two: dividing W and b by it is
+        [W_final / scale ; w_match ; 0], then lg_assign_scores: the similarity of its fp16 halves by
+        MFMA with each row's and column's logsumexp, and the combine (two launches, no framework op;
+        lightglue.py:208-233). d^0.25 = 4 for d = 256, a power of two: dividing W and b by it is
         exact unless a quotient falls below 2^-14 (fp16 subnormals), where it loses up to 2 bits; so
         the output equals the reference's fp16(final_proj(d)) / scale except for weights, biases or
         outputs that small, which differ by at most that subnormal rounding."""
@@ -496,8 +513,7 @@ class MatchAssignment(nn.Module):
 
         w, b = _cached(self, "_assign_aug", (fp.weight, fp.bias, mt.weight, mt.bias), x.dtype, build)
         v = _Hip.linear(x, w, b).view(pr, m + n, 384)
-        sim = torch.bmm(v[:, :m, :d], v[:, m:, :d].transpose(1, 2))   # fp16 [P, m, n]
-        return _Hip.log_double_softmax_f16(sim, v, m, d)
+        return _Hip.assign_scores(v, m, d)   # sim (fp16) and the dual log-softmax: two launches
 
     def forward(self, d0: torch.Tensor, d1: torch.Tensor, hip: bool = False) -> torch.Tensor:
         m0 = self.final_proj(d0) / self.scale
@@ -578,7 +594,7 @@ class LightGlueMatcher(nn.Module):
         for layer in self.transformers:
             x = layer(x, cos, sin, splits, self.attention, hip)
         head = self.log_assignment[self.n_layers - 1]
-        scores = head.forward_rows(x, pr, m, n) if hip and head.hip16_ok(x, n) else None
+        scores = head.forward_rows(x, pr, m, n) if hip and head.hip16_ok(x, m, n) else None
         x = x.view(pr, m + n, x.shape[-1])
         d0, d1 = x[:, :m], x[:, m:]
         return d0, d1, scores if scores is not None else head(d0, d1, hip)

@@ -531,8 +531,8 @@ def test_torch_glue_runs_pairs_one_by_one():
 @pytest.mark.parametrize("pairs,n0,n1", [(3, 37, 70), (2, 1000, 777), (16, 1024, 1024), (9, 1000, 1011), (40, 20, 30), (5, 1, 63),
                                          (4, 56, 1)])
 def test_wide_projections_equal_narrow(pairs, n0, n1):
-    """The projections' 256-row tile forms (csrc/lightglue_linear.hip linear_tile_kernel: 256 x 128,
-    256 x 256 and 128 x 256 tiles with the LDS-staged coalesced epilogue, taken for launches of at
+    """The projections' tile forms (csrc/lightglue_linear.hip linear_tile_kernel: 256 x 128 and
+    256 x 256 tiles on 8 waves, 128 x 128 on 4, with the LDS-staged coalesced epilogue, taken for launches of at
     least one round of tiles: several image pairs per forward) give the bits of the 64 x 64 form on
     every fused entry point — ragged row counts (rows past m in a tile: computed on the clamped last
     row, their stores rewrite that row's bytes), both K (256 and 512), residual on and off, the
@@ -576,7 +576,7 @@ def test_wide_projections_equal_narrow(pairs, n0, n1):
         try:
             narrow = [flat(o) for o in run()]
             forms = []
-            for mode in (1, 2, 3, 4, 5):  # 256 x 128; 256 x 256 (32-deep K steps); 128 x 256; 128 x 128 (4 waves)
+            for mode in (1, 2, 4):  # 256 x 128; 256 x 256 (32-deep K steps); 128 x 128 (4 waves)
                 lib.lg_linear_set_wide(mode)
                 forms.append([flat(o) for o in run()])
             torch.cuda.synchronize()
@@ -755,6 +755,42 @@ def test_ffn_rows_kernel(pairs, n0, n1):
     assert err_rows <= 2e-2 and err_two <= 2e-2
     assert torch.equal(outs[2], outs[1])  # the default: one launch
     assert torch.equal(no_pack, outs[0]) and torch.equal(packed_c, wp)  # lg_ffn_pack == ffn_pack
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pairs,m,n", [(1, 64, 48), (3, 300, 256), (1, 130, 216), (1, 1024, 1024), (16, 1024, 1024),
+                                     (2, 2048, 2000), (1, 2048, 2048), (1, 1003, 1016), (1, 1, 8), (5, 37, 1024)])
+def test_assign_scores_kernel(pairs, m, n):
+    """lg_assign_scores (the fp16 assignment head: sim = m0 · m1ᵀ by MFMA and each row's / column's exact
+    logsumexp in one launch, the combine in a second; lightglue.py:208-233) against (1) torch's fp16 bmm
+    for sim (fp32 accumulation, fp16 out: within one fp16 ulp, the accumulation order differing), (2)
+    the torch restatement of the dual log-softmax on the kernel's own sim (the workspace copy: 2e-5 of
+    the scale) and (3) that restatement on torch's sim (2 ulps of the similarity scale)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lightglue_amd import _lib
+    from lightglue_amd import matcher as mt
+
+    lib = _lib.load()
+    dev, dt = torch.device("cuda:0"), torch.float16
+    gen = torch.Generator().manual_seed(pairs * 11 + m + n)
+    with torch.no_grad():
+        v = (torch.randn(pairs, m + n, 384, generator=gen) * 0.25).to(dev, dt)
+        got = mt._Hip.assign_scores(v, m, 256)
+        ws_sim = mt._Hip._last_assign_ws[:pairs * m * n * 2].view(dt).view(pairs, m, n).clone()
+        sim_t = torch.bmm(v[:, :m, :256], v[:, m:, :256].transpose(1, 2))
+        z0, z1 = v[:, :m, 256:257].float(), v[:, m:, 256:257].float()
+        ref_own = mt.log_double_softmax(ws_sim.float(), z0, z1)
+        ref_t = mt.log_double_softmax(sim_t.float(), z0, z1)
+        torch.cuda.synchronize()
+    d_sim = (ws_sim.float() - sim_t.float()).abs()
+    ulp = torch.clamp(sim_t.float().abs(), min=2.0 ** -14) * 2.0 ** -10
+    scale = max(1.0, float(sim_t.float().abs().max()))
+    e_own, e_t = float((got - ref_own).abs().max()), float((got - ref_t).abs().max())
+    print(f"assign scores P={pairs} {m}x{n}: sim differs in {int((d_sim > 0).sum())} of {d_sim.numel()} (max "
+          f"{float(d_sim.max()):.2e}); scores vs restatement on own sim {e_own:.2e}, on torch's sim {e_t:.2e}")
+    assert bool((d_sim <= ulp).all())
+    assert torch.isfinite(got).all() and e_own <= 2e-5 * scale * 4 and e_t <= 2 * scale * 2.0 ** -10 * 4
 
 
 @pytest.mark.gpu

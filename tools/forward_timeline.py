@@ -4,7 +4,7 @@ seams inside the graph), summed by kernel family.
 
     python tools/forward_timeline.py <dir>/m_kernel_trace.csv [kernels per forward]
 
-Without a count, one forward is cut at the assignment head (lse16 + combine16, once per forward)."""
+Without a count, one forward is cut at the assignment head's combine pass (its last kernel, once per forward)."""
 import csv
 import sys
 from collections import defaultdict
@@ -13,7 +13,8 @@ from collections import defaultdict
 def family(name):
     n = name.removeprefix("void ").replace("(anonymous namespace)::", "").replace("mha_hd64::", "")
     for k in ("mha_hd64_stream_kernel", "mha_hd64_direct16_kernel", "mha_hd64_direct_kernel", "mha_hd64_fwd_kernel",
-              "linear_tile_kernel", "linear_kernel", "linear_ln_kernel", "ln_gelu", "lse16", "combine16", "pair_inputs", "Cijk"):
+              "linear_tile_kernel", "linear_kernel", "linear_ln_kernel", "ffn_rows_kernel", "assign_lse_kernel",
+              "assign_combine_kernel", "ln_gelu", "lse16", "combine16", "pair_inputs", "Cijk"):
         if k in n:
             if k.startswith("linear") and k != "linear_ln_kernel":
                 return n.split("(")[0]
@@ -27,12 +28,9 @@ def main():
     per = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     if per:
         last = rows[-per:]
-    else:  # one forward = the kernels after the second-to-last assignment head (lse16, once per forward)
-        marks = [i for i, n in enumerate(names) if "lse16" in n]
+    else:  # one forward = the kernels after the second-to-last forward's last kernel (its combine pass)
+        marks = [i for i, n in enumerate(names) if "assign_combine" in n or "combine16" in n]
         last = rows[marks[-2] + 1:marks[-1] + 1] if len(marks) >= 2 else rows
-        # (the last forward's head is followed by its combine pass)
-        last += [r for r in rows[marks[-1] + 1:marks[-1] + 2] if "combine16" in r["Kernel_Name"]]
-        last = last[1:] if last and "combine16" in last[0]["Kernel_Name"] else last
         per = len(last)
     t0 = int(last[0]["Start_Timestamp"])
     t1 = int(last[-1]["End_Timestamp"])
