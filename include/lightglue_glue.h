@@ -102,15 +102,36 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
 int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
                           int32_t pairs, const void* w1, const void* b1, const void* gamma, const void* beta, float eps,
                           const void* w2, const void* b2, const void* w_packed, void* h, void* out, hipStream_t stream);
-/* lg_ffn_pack:          W1 [2d, 2d] and W2 [d, 2d] (nn.Linear layout, fp16, d = heads*64 = 256) re-laid as
- *                       the one-launch FFN reads them: 8 wave streams of 96 KiB, stream w = 64 KiB of W1
- *                       rows 64w..64w+63 then 32 KiB of W2 rows 32w..32w+31, in 1-KiB pieces i (W1: step j,
- *                       block b at i = 2j + b; W2: step j at i = 64 + j) whose 16-B lane l holds
- *                       W[row0 + 32b + (l % 32)][16j + 8(l / 32) .. + 8] — every load of the kernel one
- *                       contiguous KiB. lg_ffn_packed_bytes(heads): its size (786,432 B; 0 if heads != 4).
- *                       Weights are static: pack once per weight update. */
-size_t lg_ffn_packed_bytes(int32_t heads);
-int32_t lg_ffn_pack(const void* w1, const void* w2, int32_t heads, void* packed, hipStream_t stream);
+/* lg_ffn_pack:          W1 [2d, 2d] and W2 [d, 2d] (nn.Linear layout, fp16, d = heads*64 = 256), and for
+ *                       lg_linear_cat_ffn_proj a W3 [n3, d] (n3 = 512 or 768; 0: none), re-laid as the
+ *                       one-launch FFN reads them: 8 wave streams of (96 + n3/16) KiB, stream w = W1 rows
+ *                       64w..64w+63 then W2 rows 32w..32w+31 then W3 rows (n3/8)w.., in 1-KiB pieces i
+ *                       (W1: step j, block b at i = 2j + b; W2: step j at i = 64 + j; W3: step j, block b at
+ *                       i = 96 + (n3/256) j + b) whose 16-B lane l holds W[row0 + 32b + (l % 32)][16j + 8(l / 32)
+ *                       .. + 8] — every load of the kernel one contiguous KiB. lg_ffn_packed_bytes(heads, n3):
+ *                       its size (786,432 B for n3 = 0; 0 if heads != 4 or n3 is not 0 / 512 / 768).
+ *                       Weights are static: pack once per weight update. lg_linear_cat_ffn takes an n3 = 0 pack. */
+size_t lg_ffn_packed_bytes(int32_t heads, int32_t n3);
+int32_t lg_ffn_pack(const void* w1, const void* w2, const void* w3, int32_t n3, int32_t heads, void* packed,
+                    hipStream_t stream);
+/* lg_linear_cat_ffn_proj: lg_linear_cat_ffn's one-launch form, then — in the same launch, on its output
+ *                       out = x' still in LDS — the projection the next attention needs (bitwise the
+ *                       separate call's outputs; round 6):
+ *                         kind LG_PROJ_SPLIT2: W3 = [W_qk; W_v] [512, d], b3 [512] -> a0, a1, b0, b1 as
+ *                                              lg_linear_split2 (outs3[0..3]);
+ *                         kind LG_PROJ_QKV:    W3 = Wqkv permuted [768, d], b3 [768], cos / sin [m, 64] ->
+ *                                              q0, k0, v0, q1, k1, v1 as lg_linear_qkv_rotary (outs3[0..5]);
+ *                         kind LG_PROJ_PLAIN:  W3 [512, d] (rows past n_store zero), b3 [512] -> outs3[0]
+ *                                              [m, n_store] = x' · W3ᵀ + b3 (n_store <= 512, % 8 == 0).
+ *                       w_packed = lg_ffn_pack(W1, W2, W3, 512 or 768); out [m, d] as lg_linear_cat_ffn
+ *                       (all pointers 16-B aligned but b3 / cos / sin, 8-B). heads must be 4. */
+#define LG_PROJ_SPLIT2 1
+#define LG_PROJ_QKV 2
+#define LG_PROJ_PLAIN 3
+int32_t lg_linear_cat_ffn_proj(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
+                               int32_t pairs, const void* b1, const void* gamma, const void* beta, float eps, const void* b2,
+                               const void* w_packed, int32_t kind, const void* b3, const void* cosv, const void* sinv,
+                               int32_t n_store, void* const* outs3, void* out, hipStream_t stream);
 /* lg_linear_qkv_rotary: SelfBlock projection (lightglue.py:111-134) with W's rows and the bias in
  *                       [q|k|v][head][dim] order (row j*heads*64 + h*64 + d = Wqkv row (h*64+d)*3 + j):
  *                       rotary (cos/sin [n0+n1, 64]) on q and k in fp16 arithmetic, as the reference's
@@ -142,14 +163,15 @@ int32_t lg_log_double_softmax_f16(const void* sim, const void* z0, const void* z
                                   int64_t z_row_stride, int32_t m, int32_t n, int32_t batch, float* scores,
                                   void* workspace, hipStream_t stream);
 
-/* The fp16 assignment head in two launches (round 6): v [batch][m + n][ld] fp16 is the final
+/* The fp16 assignment head in three launches (round 6): v [batch][m + n][ld] fp16 is the final
  * projection of both images' rows (image 0's m rows, then image 1's n; pairs pair_stride elements
  * apart), channels 0..255 the scaled descriptors m0 / m1 (final_proj(d) / d^0.25) and channel zc
  * (>= 256) the matchability logit. scores [batch, m, n] fp32 = log_softmax(sim, 2) + log_softmax(sim, 1)
  * + logsig(z0) + logsig(z1)ᵀ with sim = m0 · m1ᵀ rounded to fp16 (lightglue.py:208-233): the similarity
- * by MFMA and each row's and column's exact logsumexp in one launch (a workgroup owns 32 rows of one
- * image against all of the other), the combine in a second. m, n <= 2048, n % 8 == 0, ld % 8 == 0;
- * v, scores, workspace 16-B aligned; workspace >= lg_assign_scores_workspace(m, n, batch) bytes. */
+ * by MFMA with each row's and column's (max, sum of exponentials) over shares of the other image (a
+ * workgroup owns 32 rows of one image), the logsumexps closed once per row and column, the combine.
+ * m, n <= 2048, n % 8 == 0, ld % 8 == 0; v, scores, workspace 16-B aligned; workspace >=
+ * lg_assign_scores_workspace(m, n, batch) bytes (its first batch * m * n * 2 bytes: sim, fp16). */
 size_t lg_assign_scores_workspace(int32_t m, int32_t n, int32_t batch);
 int32_t lg_assign_scores(const void* v, int64_t pair_stride, int32_t ld, int32_t zc, int32_t m, int32_t n, int32_t batch,
                          float* scores, void* workspace, hipStream_t stream);

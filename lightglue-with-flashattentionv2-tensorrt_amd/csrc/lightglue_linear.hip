@@ -875,7 +875,15 @@ constexpr int kFfnOut = 256;  // the FFN's output channels (d)
 // Arithmetic: the k16 blocks in the 64 x 64 form's order; h = fp16(acc + b1) in one rounding, the
 // LayerNorm statistics as lg_layernorm_gelu forms them (sum and sum of squares, fixed reduction order),
 // normalisation and GELU as linear_ln_kernel, the output fp16(fp16(acc + b2) + x) as lin_val / res_add.
-constexpr int kFfnPackedBytes = (512 * 512 + 256 * 512) * 2;  // lg_ffn_pack: 8 wave streams of 96 KiB
+// phase 3 (lg_linear_cat_ffn_proj): the next attention's projection of the FFN output x'
+enum { E3_NONE = 0, E3_SPLIT2 = 1, E3_QKV = 2, E3_PLAIN = 3 };
+struct Proj3 {
+    const f16* b3;      // [n3] bias
+    const f16* cosv;    // E3_QKV: rotary tables [m, 64]
+    const f16* sinv;
+    f16* out[6];        // SPLIT2: a0 a1 b0 b1; QKV: q0 k0 v0 q1 k1 v1 (per-image head-major); PLAIN: [m, n_store]
+    int n_store;        // E3_PLAIN: channels stored per row (the first n_store of 32 NB3 8)
+};
 // Diagnostic build (-DLG_FR_STAMPS, tools/fr_stamps.py; never shipped): per wave of the first 256
 // workgroups, s_memtime cycles of chained segments (0 entry -> A in LDS, 1 phase 1, 2 LayerNorm + GELU,
 // 3 phase 2, 4 epilogue), read back by lg_diag_fr_stamps.
@@ -893,10 +901,11 @@ __device__ unsigned long long g_fr_stamps[256 * 8 * 8];
     do {          \
     } while (0)
 #endif
-template <int MB, int D>
+template <int MB, int D, int E3, int NB3>
 __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* __restrict__ gamma,
                                                           const f16* __restrict__ beta, float eps,
-                                                          const f16* __restrict__ wp, const f16* __restrict__ b2) {
+                                                          const f16* __restrict__ wp, const f16* __restrict__ b2,
+                                                          Proj3 q3) {
     constexpr int MT = 32 * MB;                    // rows per workgroup
     constexpr int K = 512, NO = kFfnOut;           // FFN width (= hidden), output channels
     constexpr int kA = 0, kH = MT * K * 2;         // A and h tiles, [MT][1 KiB] each
@@ -905,9 +914,17 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
     constexpr int kPar = MB == 1 ? kStg + 8 * MT * kSP : 2 * kH;  // b1, gamma, beta [512], b2 [256] fp16
     constexpr int kRed = kPar + (3 * K + NO) * 2;  // row partials [2][MT][8 waves] fp32
     constexpr int NS1 = K / 16, NS = 2 * NS1;      // k16 steps per GEMM; the stream: phase 1, then 2
-    static_assert(D >= 1 && D <= NS1 && (MB == 1 || MB == 2), "shape");
+    constexpr int NS3 = NO / 16;                   // phase 3: k16 steps over x' (K = 256)
+    constexpr int NP = 96 + NB3 * NS3;             // the wave's stream: pieces of 1 KiB
+    constexpr int R = 2 * D;                       // pieces in flight (a register ring)
+    static_assert(D >= 1 && D <= NS1 && (MB == 1 || MB == 2) && (E3 == E3_NONE) == (NB3 == 0), "shape");
     static_assert(MB == 1 || 8 * MT * kSP <= kH, "staging over h");
-    __shared__ __attribute__((aligned(16))) char smem[kRed + 2 * MT * 8 * 4];
+    // phase 3's vectors, loaded with A: b3 [32 NB3 8] fp16 and (E3_QKV) this tile's rows of cos / sin
+    constexpr int kB3 = kRed + 2 * MT * 8 * 4;
+    constexpr int kCS = kB3 + NB3 * 256 * 2;           // [2][MT][64] fp16
+    constexpr int kEnd = kCS + (E3 == E3_QKV ? 2 * MT * kD * 2 : 0);
+    static_assert(kEnd <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) char smem[kEnd];
     lds_char* const lds = (lds_char*)smem;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -941,6 +958,20 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
         pv = *reinterpret_cast<const f16x8*>(pvs + (tid & 63) * 8);
     }
 
+    constexpr int NV3 = NB3 * 256 * 2 / 16 + (E3 == E3_QKV ? 2 * MT * kD * 2 / 16 : 0);  // 16-B units
+    constexpr int NV3T = (NV3 + 511) / 512;
+    f16x8 v3[NV3T > 0 ? NV3T : 1];
+#pragma unroll
+    for (int i = 0; i < NV3T; ++i) {
+        const int u = i * 512 + tid;
+        if (u < NB3 * 256 * 2 / 16) {
+            v3[i] = *reinterpret_cast<const f16x8*>(q3.b3 + u * 8);
+        } else if (u < NV3) {  // cos / sin rows: table t, row rw (clamped), unit cu
+            const int cu = u - NB3 * 256 * 2 / 16, t = cu / (MT * 8), rw = min(m0 + (cu % (MT * 8)) / 8, p.m - 1);
+            v3[i] = *reinterpret_cast<const f16x8*>((t ? q3.sinv : q3.cosv) + (size_t)rw * kD + (cu % 8) * 8);
+        }
+    }
+
     // every wave's A loads are issued before any wave's weight stream: the loads of a CU pass its
     // texture unit in issue order, and A behind seven waves' weight prefetch waited ~2.6 k cycles
     asm volatile("s_barrier" ::: "memory");
@@ -949,19 +980,20 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
     // lane l's 16 B at + 16 l: step j of phase 1, block b = piece 2 j + b; step j of phase 2 = 64 + j.
     // Every load is one contiguous KiB (whole 128-B lines: the row-major W's 32-B row pieces per
     // lane fetched each line four times, 26 vs 12 us per launch at 2,048 rows) ----
-    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(wp), (short)0, kFfnPackedBytes, 0x00020000);
-    const unsigned wo = (unsigned)(wave * (kFfnPackedBytes / 8) + lane * 16);
-    auto wfrag = [&](int j, int b) {
-        const int i = j < NS1 ? 2 * j + b : NS1 + j;
-        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, wo, i * 1024, 0));
-    };
-    f16x8 q[D][2];
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(wp), (short)0, 8 * NP * 1024, 0x00020000);
+    const unsigned wo = (unsigned)(wave * NP * 1024 + lane * 16);
+    auto piece = [&](int i) { return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, wo, i * 1024, 0)); };
+    f16x8 q[R];  // piece i in slot i % R; consuming piece i issues piece i + R
 #pragma unroll
-    for (int j = 0; j < D; ++j) {  // (in stream order: the loop's counted waits assume it)
-        q[j][0] = wfrag(j, 0);
-        q[j][1] = wfrag(j, 1);
-        __builtin_amdgcn_sched_barrier(0);
+    for (int i = 0; i < R; ++i) {  // (in stream order: the loops' counted waits assume it)
+        q[i] = piece(i);
+        if (i & 1) __builtin_amdgcn_sched_barrier(0);
     }
+    auto take = [&](int i) {  // piece i (compile-time after unrolling), and the refill behind it
+        const f16x8 w = q[i % R];
+        if (i + R < NP) q[i % R] = piece(i + R);
+        return w;
+    };
     // A and the vectors into LDS (the compiler's wait counts the weight loads issued after them)
 #pragma unroll
     for (int i = 0; i < 4 * MB; ++i) {
@@ -969,6 +1001,9 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
         *(lds_f16x8*)(lds + kA + row * 1024 + ((lane ^ (row & 15)) << 4)) = av[i];
     }
     if (tid < 224) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
+#pragma unroll
+    for (int i = 0; i < NV3T; ++i)
+        if (i * 512 + tid < NV3) *(lds_f16x8*)(lds + kB3 + (i * 512 + tid) * 16) = v3[i];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     FR_SEG(0);
@@ -992,11 +1027,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
     BF af = bfrag(kA, 0);
 #pragma unroll
     for (int j = 0; j < NS1; ++j) {
-        const f16x8 wa = q[j % D][0], wb = q[j % D][1];
-        if (j + D < NS) {
-            q[j % D][0] = wfrag(j + D, 0);
-            if (j + D < NS1) q[j % D][1] = wfrag(j + D, 1);
-        }
+        const f16x8 wa = take(2 * j), wb = take(2 * j + 1);
         const BF an = j + 1 < NS1 ? bfrag(kA, j + 1) : af;
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) {
@@ -1083,8 +1114,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
     BF hf = bfrag(kH, 0);
 #pragma unroll
     for (int j = NS1; j < NS; ++j) {
-        const f16x8 wa = q[j % D][0];
-        if (j + D < NS) q[j % D][0] = wfrag(j + D, 0);
+        const f16x8 wa = take(NS1 + j);
         const BF hn = j + 1 < NS ? bfrag(kH, j + 1 - NS1) : hf;
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) o2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa, hf.v[mb], o2[mb], 0, 0, 0);
@@ -1111,39 +1141,144 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
             *(__attribute__((address_space(3))) f16x4*)(stg + (32 * mb + r) * kSP + (8 * g + 4 * hh) * 2) = v;
         }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the wave's own rows: LDS ops of a wave in order)
+    f16x8 xo[MB][2];  // x' = this lane's out values (phase 3's input)
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
         const int rr = 32 * mb + (lane >> 1), half = lane & 1;
-        if (m0 + rr < p.m) {
 #pragma unroll
-            for (int e2 = 0; e2 < 2; ++e2) {
-                f16x8 v = *(lds_f16x8*)(stg + rr * kSP + half * 32 + e2 * 16);
-                const f16x8 xr = *(lds_f16x8*)(lds + kA + rr * 1024 + (((4 * wave + 2 * half + e2) ^ (rr & 15)) << 4));
+        for (int e2 = 0; e2 < 2; ++e2) {
+            f16x8 v = *(lds_f16x8*)(stg + rr * kSP + half * 32 + e2 * 16);
+            const f16x8 xr = *(lds_f16x8*)(lds + kA + rr * 1024 + (((4 * wave + 2 * half + e2) ^ (rr & 15)) << 4));
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], xr[e]);
-                *reinterpret_cast<f16x8*>(p.out[0] + (size_t)(m0 + rr) * NO + 32 * wave + 16 * half + 8 * e2) = v;
-            }
+            for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], xr[e]);
+            xo[mb][e2] = v;
+            if (m0 + rr < p.m) *reinterpret_cast<f16x8*>(p.out[0] + (size_t)(m0 + rr) * NO + 32 * wave + 16 * half + 8 * e2) = v;
         }
     }
 #ifdef LG_FR_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     FR_SEG(4);
+#endif
+    if constexpr (E3 != E3_NONE) {
+        // ---- phase 3: the next projection of x' (K = 256): x' rows into the A region ([MT][512 B],
+        // units XOR (row & 15)) once every wave has read its residual there ----
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+            const int rr = 32 * mb + (lane >> 1), half = lane & 1;
+#pragma unroll
+            for (int e2 = 0; e2 < 2; ++e2)
+                *(lds_f16x8*)(lds + kA + rr * 512 + (((4 * wave + 2 * half + e2) ^ (rr & 15)) << 4)) = xo[mb][e2];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        auto xfrag = [&](int s) {
+            BF f;
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb) {
+                const int row = 32 * mb + r;
+                f.v[mb] = *(lds_f16x8*)(lds + kA + row * 512 + (((2 * s + hh) ^ (row & 15)) << 4));
+            }
+            return f;
+        };
+        // the wave's NB3 blocks of 32 output channels, c = 32 (NB3 w + b) + ...
+        f32x16 a3[NB3][MB] = {};
+        BF xf = xfrag(0);
+#pragma unroll
+        for (int j = 0; j < NS3; ++j) {
+            f16x8 w3[NB3];
+#pragma unroll
+            for (int b = 0; b < NB3; ++b) w3[b] = take(96 + NB3 * j + b);
+            const BF xn = j + 1 < NS3 ? xfrag(j + 1) : xf;
+#pragma unroll
+            for (int b = 0; b < NB3; ++b)
+#pragma unroll
+                for (int mb = 0; mb < MB; ++mb) a3[b][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w3[b], xf.v[mb], a3[b][mb], 0, 0, 0);
+            xf = xn;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // epilogue: fp16(acc + b3) (+ rotary for q, k) as the standalone projections compute it, the
+        // wave's rows x 32 channels of a block staged (its own rows of the staging region), then two
+        // lanes a row, 32 B each, to the row's head-major (or row-major) destination
+#pragma unroll
+        for (int b = 0; b < NB3; ++b) {
+            const int cb = 32 * (NB3 * wave + b);  // the block's first channel (one head of one part)
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int c = cb + 8 * g + 4 * hh;
+                    const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kB3 + c * 2);
+                    f16x4 v = f16x4{lin_val(a3[b][mb][4 * g], b4[0]), lin_val(a3[b][mb][4 * g + 1], b4[1]),
+                                    lin_val(a3[b][mb][4 * g + 2], b4[2]), lin_val(a3[b][mb][4 * g + 3], b4[3])};
+                    if constexpr (E3 == E3_QKV) {
+                        if (cb < 2 * NO) {  // q, k: rotary pairs (d, d + 1) from this row's tables
+                            const int rw = 32 * mb + r;  // (tile row; rows past m hold row m - 1's tables)
+                            const f16x4 cc = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + (rw * kD + c % kD) * 2);
+                            const f16x4 ss = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + ((MT + rw) * kD + c % kD) * 2);
+#pragma unroll
+                            for (int t = 0; t < 4; t += 2) rot_pair(v, t, cc[t], ss[t], cc[t + 1], ss[t + 1]);
+                        }
+                    }
+                    *(__attribute__((address_space(3))) f16x4*)(stg + (32 * mb + r) * kSP + (8 * g + 4 * hh) * 2) = v;
+                }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb) {
+                const int rr = 32 * mb + (lane >> 1), half = lane & 1;
+                const f16x8 v0 = *(lds_f16x8*)(stg + rr * kSP + half * 32);
+                const f16x8 v1 = *(lds_f16x8*)(stg + rr * kSP + half * 32 + 16);
+                const int row = m0 + rr;
+                if (row < p.m) {
+                    f16* dst;
+                    if constexpr (E3 == E3_PLAIN) {
+                        dst = cb < q3.n_store ? q3.out[0] + (size_t)row * q3.n_store + cb + 16 * half : nullptr;
+                    } else {
+                        const int part = cb / NO, h = (cb % NO) / kD;
+                        const LinRow lr = lin_row(p, row, h);
+                        dst = q3.out[E3 == E3_QKV ? (lr.first ? 0 : 3) + part : (lr.first ? 0 : 1) + 2 * part] + lr.off +
+                              cb % kD + 16 * half;
+                    }
+                    if (dst) {
+                        *reinterpret_cast<f16x8*>(dst) = v0;
+                        *reinterpret_cast<f16x8*>(dst + 8) = v1;
+                    }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the next block rewrites the staging rows)
+        }
+    }
+#ifdef LG_FR_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FR_SEG(5);  // (phase 3 and its epilogue; segment 4 then ends at phase 2's stores)
+#endif
+#ifdef LG_FR_STAMPS
     if (lane == 0 && blockIdx.x < 256) {
         unsigned long long* d = g_fr_stamps + ((size_t)blockIdx.x * 8 + wave) * 8;
         for (int k = 0; k < 5; ++k) d[k] = fr_[k];
         d[5] = fr_last_ - fr_entry_;
         d[6] = fr_entry_;
+        d[7] = fr_[5];
     }
 #endif
 }
 
-// lg_ffn_pack: one thread per 16-B fragment of the packed stream (layout: include/lightglue_glue.h)
-__global__ __launch_bounds__(256) void ffn_pack_kernel(const f16* __restrict__ w1, const f16* __restrict__ w2, f16* packed) {
-    const int f = blockIdx.x * 256 + threadIdx.x;  // fragment: wave w = f / 6144, piece i, lane l
-    if (f >= kFfnPackedBytes / 16) return;
-    const int w = f / 6144, i = (f % 6144) / 64, l = f % 64, r = l % 32, hh = l / 32;
-    const f16* src = i < 64 ? w1 + (size_t)(64 * w + 32 * (i & 1) + r) * 512 + 16 * (i >> 1) + 8 * hh
-                            : w2 + (size_t)(32 * w + r) * 512 + 16 * (i - 64) + 8 * hh;
+// lg_ffn_pack: one thread per 16-B fragment of the packed stream (layout: include/lightglue_glue.h);
+// wave w's stream: 64 W1 pieces, 32 W2 pieces, then NB3 x 16 W3 pieces (NB3 = n3 / 256)
+__global__ __launch_bounds__(256) void ffn_pack_kernel(const f16* __restrict__ w1, const f16* __restrict__ w2,
+                                                       const f16* __restrict__ w3, int nb3, f16* packed) {
+    const int np = 96 + 16 * nb3;                  // pieces per wave
+    const int f = blockIdx.x * 256 + threadIdx.x;  // fragment: wave w, piece i, lane l
+    if (f >= 8 * np * 64) return;
+    const int w = f / (np * 64), i = (f % (np * 64)) / 64, l = f % 64, r = l % 32, hh = l / 32;
+    const f16* src;
+    if (i < 64) src = w1 + (size_t)(64 * w + 32 * (i & 1) + r) * 512 + 16 * (i >> 1) + 8 * hh;
+    else if (i < 96) src = w2 + (size_t)(32 * w + r) * 512 + 16 * (i - 64) + 8 * hh;
+    else {
+        const int j = (i - 96) / nb3, b = (i - 96) % nb3;
+        src = w3 + (size_t)(32 * (nb3 * w + b) + r) * 256 + 16 * j + 8 * hh;
+    }
     *reinterpret_cast<f16x8*>(packed + (size_t)f * 8) = *reinterpret_cast<const f16x8*>(src);
 }
 
@@ -1160,8 +1295,8 @@ __global__ __launch_bounds__(256) void ffn_pack_kernel(const f16* __restrict__ w
 //    column partials: no cross-workgroup exchange. (An image-1 workgroup recomputes its columns of sim
 //    with the operands swapped: the same products in the same k-step order.) S splits of the other
 //    image fill the chip at a single pair (each workgroup then streams 1/S of it).
-//  * assign_combine_kernel: closes the S partials of each row and column (fixed order) into the
-//    logsumexps and writes scores = 2 sim + (logsig(z0) - lse_row) + (logsig(z1) - lse_col), fp32.
+//  * assign_close_kernel closes the S partials of each row and column (fixed order) into the terms
+//    logsig(z) - logsumexp, once; assign_combine_kernel writes scores = 2 sim + row term + column term.
 struct AsArgs {
     const f16* v;     // [batch][m + n][ld]: image 0's rows then image 1's; channels 0..255 the scaled
                       // final projection, channel zc the matchability logit
@@ -1170,6 +1305,8 @@ struct AsArgs {
     f16* sim;         // workspace [batch][m][n]
     float2* rpart;    // workspace [batch][S][m]: (max, sum of exp) of row i over split s
     float2* cpart;    // workspace [batch][S][n]: the same for column j
+    float* rterm;     // workspace [batch][m]: logsig(z0[i]) - lse_row[i]
+    float* cterm;     // workspace [batch][n]: logsig(z1[j]) - lse_col[j]
     float* scores;    // [batch][m][n]
 };
 __device__ __forceinline__ float log_sigmoid_f(float z) { return fminf(z, 0.f) - log1pf(__expf(-fabsf(z))); }
@@ -1310,55 +1447,48 @@ __device__ __forceinline__ float lse_close(const float2* part, size_t stride, in
     return mx + __logf(s);
 }
 
-// scores = 2 sim + (logsig(z0[i]) - lse_row[i]) + (logsig(z1[j]) - lse_col[j]) (fp32), W waves per
-// block, 8 rows per wave, 16-B loads / stores
-template <int CPL, int W>  // columns per lane in units of 8 (n <= 512 CPL)
-__global__ __launch_bounds__(64 * W) void assign_combine_kernel(AsArgs a) {
-    const int p = blockIdx.y;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// the row and column terms once: term = logsig(z) - logsumexp closed from the S partials (one thread
+// per row of image 0, then per column)
+__global__ __launch_bounds__(256) void assign_close_kernel(AsArgs a) {
+    const int p = blockIdx.y, t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= a.m + a.n) return;
     const f16* const vp = a.v + (size_t)p * a.ps;
-    __shared__ float ct[512 * CPL];
-    for (int j = threadIdx.x; j < a.n; j += 64 * W)
-        ct[j] = log_sigmoid_f((float)vp[(size_t)(a.m + j) * a.ld + a.zc]) -
-                lse_close(a.cpart + (size_t)p * a.S * a.n + j, a.n, a.S);
-    __syncthreads();
-    const int i0 = (blockIdx.x * W + wave) * 8;
-    if (i0 >= a.m) return;
+    const float z = (float)vp[(size_t)t * a.ld + a.zc];  // (row t of v: image 0's rows, then image 1's)
+    if (t < a.m) a.rterm[(size_t)p * a.m + t] = log_sigmoid_f(z) - lse_close(a.rpart + (size_t)p * a.S * a.m + t, a.m, a.S);
+    else a.cterm[(size_t)p * a.n + t - a.m] = log_sigmoid_f(z) - lse_close(a.cpart + (size_t)p * a.S * a.n + t - a.m, a.n, a.S);
+}
+
+// scores = 2 sim + rterm[i] + cterm[j] (fp32). A block is 8 W rows x 512 columns; each wave writes 8
+// rows, a lane 8 columns (16-B loads, 2 x 16-B stores)
+template <int W>
+__global__ __launch_bounds__(64 * W) void assign_combine_kernel(AsArgs a) {
+    const int p = blockIdx.z;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i0 = (blockIdx.x * W + wave) * 8, j = blockIdx.y * 512 + lane * 8;
+    if (i0 >= a.m || j >= a.n) return;
     const int i1 = min(i0 + 8, a.m);
     const f16* sim = a.sim + (size_t)p * a.m * a.n;
     float* out = a.scores + (size_t)p * a.m * a.n;
-    f16x8 x[8][CPL];
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        const int i = min(i0 + b, i1 - 1);
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-            const int j = (c * 64 + lane) * 8;
-            if (j < a.n) x[b][c] = *reinterpret_cast<const f16x8*>(sim + (size_t)i * a.n + j);
-        }
-    }
+    f16x8 x[8];
     float rt[8];
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
         const int i = min(i0 + b, i1 - 1);
-        rt[b] = log_sigmoid_f((float)vp[(size_t)i * a.ld + a.zc]) - lse_close(a.rpart + (size_t)p * a.S * a.m + i, a.m, a.S);
+        x[b] = *reinterpret_cast<const f16x8*>(sim + (size_t)i * a.n + j);
+        rt[b] = a.rterm[(size_t)p * a.m + i];
     }
+    const f32x4 cl = *(const f32x4*)(a.cterm + (size_t)p * a.n + j), ch = *(const f32x4*)(a.cterm + (size_t)p * a.n + j + 4);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
         if (i0 + b >= i1) break;
+        f32x4 o0, o1;
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-            const int j = (c * 64 + lane) * 8;
-            if (j >= a.n) continue;
-            f32x4 o0, o1;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                o0[e] = 2.f * (float)x[b][c][e] + rt[b] + ct[j + e];
-                o1[e] = 2.f * (float)x[b][c][e + 4] + rt[b] + ct[j + e + 4];
-            }
-            *reinterpret_cast<f32x4*>(out + (size_t)(i0 + b) * a.n + j) = o0;
-            *reinterpret_cast<f32x4*>(out + (size_t)(i0 + b) * a.n + j + 4) = o1;
+        for (int e = 0; e < 4; ++e) {
+            o0[e] = 2.f * (float)x[b][e] + rt[b] + cl[e];
+            o1[e] = 2.f * (float)x[b][e + 4] + rt[b] + ch[e];
         }
+        *reinterpret_cast<f32x4*>(out + (size_t)(i0 + b) * a.n + j) = o0;
+        *reinterpret_cast<f32x4*>(out + (size_t)(i0 + b) * a.n + j + 4) = o1;
     }
 }
 
@@ -1487,6 +1617,19 @@ int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, what, hipGetErrorString(e));
 }
 
+// ffn_rows_kernel by size: 32-row workgroups up to one round of them (the most workgroups: latency),
+// 64-row beyond (half the weight bytes per row)
+template <int E3, int NB3>
+void launch_ffn_rows(const LinArgs& p, const f16* gamma, const f16* beta, float eps, const f16* wp, const f16* b2,
+                     const Proj3& q3, hipStream_t stream) {
+    if (p.m <= 32 * kTileGrid)
+        hipLaunchKernelGGL((ffn_rows_kernel<1, kFrDepth, E3, NB3>), dim3((p.m + 31) / 32), dim3(512), 0, stream, p, gamma, beta,
+                           eps, wp, b2, q3);
+    else
+        hipLaunchKernelGGL((ffn_rows_kernel<2, kFrDepth, E3, NB3>), dim3((p.m + 63) / 64), dim3(512), 0, stream, p, gamma, beta,
+                           eps, wp, b2, q3);
+}
+
 bool shape_ok(int m, int n, int k) { return m >= 0 && n > 0 && n % kBN == 0 && (k == 256 || k == 512); }
 
 int32_t bad(const char* what) { return mha_hd64::report_error(MHA_HD64_STATUS_BAD_PARAM, what, "bad arguments"); }
@@ -1580,26 +1723,57 @@ int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int
     p.a = (const f16*)x, p.ctx0 = (const f16*)ctx0, p.ctx1 = (const f16*)ctx1, p.w = (const f16*)w1;
     p.bias = (const f16*)b1, p.out[0] = (f16*)out;
     p.m = m, p.n = k, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
-    if (m <= 32 * kTileGrid)  // one round of 32-row workgroups: the most workgroups (latency)
-        hipLaunchKernelGGL((ffn_rows_kernel<1, kFrDepth>), dim3((m + 31) / 32), dim3(512), 0, stream, p, (const f16*)gamma,
-                           (const f16*)beta, eps, (const f16*)w_packed, (const f16*)b2);
-    else  // several rounds: 64 rows a workgroup, half the weight bytes per row
-        hipLaunchKernelGGL((ffn_rows_kernel<2, kFrDepth>), dim3((m + 63) / 64), dim3(512), 0, stream, p, (const f16*)gamma,
-                           (const f16*)beta, eps, (const f16*)w_packed, (const f16*)b2);
+    launch_ffn_rows<E3_NONE, 0>(p, (const f16*)gamma, (const f16*)beta, eps, (const f16*)w_packed, (const f16*)b2, Proj3{}, stream);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_linear_cat_ffn", hipGetErrorString(e));
 }
 
-size_t lg_ffn_packed_bytes(int32_t heads) { return heads == 4 ? (size_t)kFfnPackedBytes : 0; }
+size_t lg_ffn_packed_bytes(int32_t heads, int32_t n3) {
+    return heads == 4 && (n3 == 0 || n3 == 512 || n3 == 768) ? (size_t)8 * (96 + n3 / 16) * 1024 : 0;
+}
 
-int32_t lg_ffn_pack(const void* w1, const void* w2, int32_t heads, void* packed, hipStream_t stream) {
-    if (heads != 4 || !w1 || !w2 || !packed || !aligned16(w1) || !aligned16(w2) || !aligned16(packed)) return bad("lg_ffn_pack");
-    hipLaunchKernelGGL(ffn_pack_kernel, dim3(kFfnPackedBytes / 16 / 256), dim3(256), 0, stream, (const f16*)w1, (const f16*)w2,
-                       (f16*)packed);
+int32_t lg_ffn_pack(const void* w1, const void* w2, const void* w3, int32_t n3, int32_t heads, void* packed, hipStream_t stream) {
+    if (!lg_ffn_packed_bytes(heads, n3) || !w1 || !w2 || !packed || !aligned16(w1) || !aligned16(w2) || !aligned16(packed) ||
+        (n3 && (!w3 || !aligned16(w3))))
+        return bad("lg_ffn_pack");
+    const int nb3 = n3 / 256, frags = 8 * (96 + 16 * nb3) * 64;
+    hipLaunchKernelGGL(ffn_pack_kernel, dim3((frags + 255) / 256), dim3(256), 0, stream, (const f16*)w1, (const f16*)w2,
+                       (const f16*)w3, nb3, (f16*)packed);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_ffn_pack", hipGetErrorString(e));
+}
+
+int32_t lg_linear_cat_ffn_proj(const void* x, const void* ctx0, const void* ctx1, int32_t heads, int32_t n0, int32_t n1,
+                               int32_t pairs, const void* b1, const void* gamma, const void* beta, float eps, const void* b2,
+                               const void* w_packed, int32_t kind, const void* b3, const void* cosv, const void* sinv,
+                               int32_t n_store, void* const* outs3, void* out, hipStream_t stream) {
+    const int d = heads * kD, k = 2 * d, m = pairs * (n0 + n1);
+    const int nouts = kind == LG_PROJ_SPLIT2 ? 4 : kind == LG_PROJ_QKV ? 6 : kind == LG_PROJ_PLAIN ? 1 : 0;
+    bool ok = heads == 4 && n0 >= 0 && n1 >= 0 && pairs >= 0 && nouts && x && b1 && gamma && beta && b2 && w_packed && b3 && outs3 &&
+              out && out != x && aligned16(x) && (!n0 || aligned16(ctx0)) && (!n1 || aligned16(ctx1)) && aligned16(b1) &&
+              aligned16(gamma) && aligned16(beta) && aligned16(b2) && aligned16(w_packed) && aligned8(b3) && aligned16(out) &&
+              eps >= 0.f && (kind != LG_PROJ_QKV || (cosv && sinv && aligned8(cosv) && aligned8(sinv))) &&
+              (kind != LG_PROJ_PLAIN || (n_store > 0 && n_store <= 512 && n_store % 8 == 0)) &&
+              (kind == LG_PROJ_PLAIN || (long long)m * heads * kD < (1LL << 31));
+    for (int i = 0; ok && i < nouts; ++i) ok = outs3[i] && aligned16(outs3[i]);
+    if (!ok) return bad("lg_linear_cat_ffn_proj");
+    if (m == 0) return MHA_HD64_STATUS_SUCCESS;
+    LinArgs p{};
+    p.a = (const f16*)x, p.ctx0 = (const f16*)ctx0, p.ctx1 = (const f16*)ctx1, p.w = nullptr;
+    p.bias = (const f16*)b1, p.out[0] = (f16*)out;
+    p.m = m, p.n = k, p.k = k, p.heads = heads, p.n0 = n0, p.n1 = n1;
+    Proj3 q3{};
+    q3.b3 = (const f16*)b3, q3.cosv = (const f16*)cosv, q3.sinv = (const f16*)sinv, q3.n_store = n_store;
+    for (int i = 0; i < nouts; ++i) q3.out[i] = (f16*)outs3[i];
+    const f16 *g = (const f16*)gamma, *be = (const f16*)beta, *wp = (const f16*)w_packed, *bb2 = (const f16*)b2;
+    if (kind == LG_PROJ_SPLIT2) launch_ffn_rows<E3_SPLIT2, 2>(p, g, be, eps, wp, bb2, q3, stream);
+    else if (kind == LG_PROJ_QKV) launch_ffn_rows<E3_QKV, 3>(p, g, be, eps, wp, bb2, q3, stream);
+    else launch_ffn_rows<E3_PLAIN, 2>(p, g, be, eps, wp, bb2, q3, stream);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
+                           : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_linear_cat_ffn_proj", hipGetErrorString(e));
 }
 
 namespace {
@@ -1615,7 +1789,8 @@ int assign_splits(int32_t m, int32_t n, int32_t batch) {
 size_t lg_assign_scores_workspace(int32_t m, int32_t n, int32_t batch) {
     if (m <= 0 || n <= 0 || batch <= 0) return 0;
     const size_t b = (size_t)batch, S = (size_t)assign_splits(m, n, batch);
-    return (b * m * n * 2 + 255) / 256 * 256 + (b * S * m * 8 + 255) / 256 * 256 + (b * S * n * 8 + 255) / 256 * 256;
+    return (b * m * n * 2 + 255) / 256 * 256 + (b * S * m * 8 + 255) / 256 * 256 + (b * S * n * 8 + 255) / 256 * 256 +
+           (b * m * 4 + 255) / 256 * 256 + (b * n * 4 + 255) / 256 * 256;
 }
 
 int32_t lg_assign_scores(const void* v, int64_t pair_stride, int32_t ld, int32_t zc, int32_t m, int32_t n, int32_t batch,
@@ -1634,6 +1809,8 @@ int32_t lg_assign_scores(const void* v, int64_t pair_stride, int32_t ld, int32_t
     a.sim = (f16*)ws;
     a.rpart = (float2*)(ws + (b * m * n * 2 + 255) / 256 * 256);
     a.cpart = (float2*)((char*)a.rpart + (b * S * m * 8 + 255) / 256 * 256);
+    a.rterm = (float*)((char*)a.cpart + (b * S * n * 8 + 255) / 256 * 256);
+    a.cterm = (float*)((char*)a.rterm + (b * m * 4 + 255) / 256 * 256);
     a.scores = scores;
     const dim3 g1(a.rb0 + (n + 31) / 32, batch, a.S);
     const int oth = m > n ? m : n;  // other-image blocks per wave: ceil(blocks / (8 S))
@@ -1642,21 +1819,13 @@ int32_t lg_assign_scores(const void* v, int64_t pair_stride, int32_t ld, int32_t
     else if (bpw <= 2) hipLaunchKernelGGL(assign_lse_kernel<2>, g1, dim3(512), 0, stream, a);
     else if (bpw <= 4) hipLaunchKernelGGL(assign_lse_kernel<4>, g1, dim3(512), 0, stream, a);
     else hipLaunchKernelGGL(assign_lse_kernel<8>, g1, dim3(512), 0, stream, a);
-    // combine: 8 rows per wave; 8-wave blocks where they fill the chip, else one wave per block
-    const bool small = (long)((m + 63) / 64) * batch < 256;
-    const int W = small ? 1 : 8;
-    const dim3 g2((m + 8 * W - 1) / (8 * W), batch);
-#define LG_AC(CPL)                                                                                          \
-    if (small) hipLaunchKernelGGL((assign_combine_kernel<CPL, 1>), g2, dim3(64), 0, stream, a);             \
-    else hipLaunchKernelGGL((assign_combine_kernel<CPL, 8>), g2, dim3(512), 0, stream, a);
-    if (n <= 512) {
-        LG_AC(1)
-    } else if (n <= 1024) {
-        LG_AC(2)
-    } else {
-        LG_AC(4)
-    }
-#undef LG_AC
+    hipLaunchKernelGGL(assign_close_kernel, dim3((m + n + 255) / 256, batch), dim3(256), 0, stream, a);
+    // combine: blocks of 8 W rows x 512 columns (W = 4: 32 rows; 1 where that leaves the chip idle)
+    const int cb = (n + 511) / 512;
+    if ((long)((m + 31) / 32) * cb * batch >= 128)
+        hipLaunchKernelGGL(assign_combine_kernel<4>, dim3((m + 31) / 32, cb, batch), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL(assign_combine_kernel<1>, dim3((m + 7) / 8, cb, batch), dim3(64), 0, stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_assign_scores", hipGetErrorString(e));

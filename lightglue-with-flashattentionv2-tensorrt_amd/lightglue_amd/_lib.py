@@ -134,10 +134,12 @@ SIGNATURES.update({
     "lg_linear_cat": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P, _P], _I),
     "lg_linear_cat_ln_gelu": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, ctypes.c_float, _P, _P], _I),
     "lg_linear_cat_ffn": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, ctypes.c_float, _P, _P, _P, _P, _P, _P], _I),
-    "lg_ffn_packed_bytes": ([_I], _S),
+    "lg_ffn_packed_bytes": ([_I, _I], _S),
     "lg_assign_scores_workspace": ([_I, _I, _I], _S),
     "lg_assign_scores": ([_P, ctypes.c_int64, _I, _I, _I, _I, _I, _P, _P, _P], _I),
-    "lg_ffn_pack": ([_P, _P, _I, _P, _P], _I),
+    "lg_ffn_pack": ([_P, _P, _P, _I, _I, _P, _P], _I),
+    "lg_linear_cat_ffn_proj": ([_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, ctypes.c_float, _P, _P, _I, _P, _P, _P, _I,
+                                ctypes.POINTER(_P), _P, _P], _I),
     "lg_linear_qkv_rotary": ([_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P], _I),
     "lg_linear_split2": ([_P, _P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P], _I),
     "lg_layernorm_gelu": ([_I, _P, _P, _P, _I, _I, ctypes.c_float, _P, _P], _I),

@@ -25,6 +25,8 @@ What is different, and why:
 """
 from __future__ import annotations
 
+import ctypes
+import os
 import zlib
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -137,6 +139,36 @@ class _Hip:
                                            out.data_ptr(), _Hip._stream(x))
         _check(st, "lg_linear_cat_ffn")
         return out
+
+    @staticmethod
+    def ffn_proj(x, c0, c1, b, ln: nn.LayerNorm, b2, packed, kind, b3, splits, cos=None, sin=None, n_store=0):
+        """lg_linear_cat_ffn_proj: (x' = x + ffn([x | merge_heads(c0, c1)]), the next projection of x')
+        in one launch; kind 1 -> ((a0, a1), (b0, b1)) per-image heads (to_qk | to_v), kind 2 -> q/k/v
+        per image with the rotary, kind 3 -> [1, M, n_store] rows."""
+        n0, n1, pr = _sp(splits)
+        heads = c0.shape[1]
+        m = pr * (n0 + n1)
+        out = torch.empty((1, m, 256), dtype=x.dtype, device=x.device)
+        mk = lambda n: torch.empty((pr, heads, n, 64), dtype=x.dtype, device=x.device)  # noqa: E731
+        if kind == 1:
+            outs = [mk(n0), mk(n1), mk(n0), mk(n1)]
+        elif kind == 2:
+            outs = [mk(n0), mk(n0), mk(n0), mk(n1), mk(n1), mk(n1)]
+        else:
+            outs = [torch.empty((1, m, n_store), dtype=x.dtype, device=x.device)]
+        ptrs = (ctypes.c_void_p * 6)(*([t.data_ptr() for t in outs] + [None] * (6 - len(outs))))
+        st = _lib.load().lg_linear_cat_ffn_proj(x.data_ptr(), c0.data_ptr(), c1.data_ptr(), heads, n0, n1, pr, b.data_ptr(),
+                                                ln.weight.data_ptr(), ln.bias.data_ptr(), float(ln.eps), b2.data_ptr(),
+                                                packed.data_ptr(), kind, b3.data_ptr(),
+                                                cos.data_ptr() if cos is not None else None,
+                                                sin.data_ptr() if sin is not None else None, n_store, ptrs, out.data_ptr(),
+                                                _Hip._stream(x))
+        _check(st, "lg_linear_cat_ffn_proj")
+        if kind == 1:
+            return out, ((outs[0], outs[1]), (outs[2], outs[3]))
+        if kind == 2:
+            return out, [tuple(outs[:3]), tuple(outs[3:])]
+        return out, outs[0]
 
     @staticmethod
     def linear_cat_ln_gelu(x, c0, c1, w, b, ln: nn.LayerNorm):
@@ -278,24 +310,38 @@ def _ffn_in_fused(block: nn.Module, proj: nn.Linear, dtype: torch.dtype):
     return _cached(block, "_ffn_in_fused", (lin.weight, lin.bias, proj.weight, proj.bias), dtype, build)
 
 
-def ffn_pack(w1: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
+def ffn_pack(w1: torch.Tensor, w2: torch.Tensor, w3: Optional[torch.Tensor] = None) -> torch.Tensor:
     """The one-launch FFN's weight stream (lg_ffn_pack, include/lightglue_glue.h) by tensor ops: for
-    wave w of 8, W1 rows 64w.. as pieces (step j, block b) then W2 rows 32w.. as pieces (step j), each
-    piece's 16-B lane l = W[row0 + 32b + l % 32][16j + 8(l // 32) : + 8]."""
+    wave w of 8, W1 rows 64w.. as pieces (step j, block b), then W2 rows 32w.. as pieces (step j), then
+    (lg_linear_cat_ffn_proj) W3 rows (n3/8)w.. as pieces (step j, block b); each piece's 16-B lane l =
+    W[row0 + 32b + l % 32][16j + 8(l // 32) : + 8]."""
     p1 = w1.reshape(8, 2, 32, 32, 2, 8).permute(0, 3, 1, 4, 2, 5)   # (w, j, b, hh, r, e)
     p2 = w2.reshape(8, 32, 32, 2, 8).permute(0, 2, 3, 1, 4)         # (w, j, hh, r, e)
-    return torch.cat((p1.reshape(8, -1), p2.reshape(8, -1)), 1).reshape(-1).contiguous()
+    parts = [p1.reshape(8, -1), p2.reshape(8, -1)]
+    if w3 is not None:
+        nb3 = w3.shape[0] // 256
+        parts.append(w3.reshape(8, nb3, 32, 16, 2, 8).permute(0, 3, 1, 4, 2, 5).reshape(8, -1))  # (w, j, b, hh, r, e)
+    return torch.cat(parts, 1).reshape(-1).contiguous()
 
 
-def _ffn_packed(block: nn.Module, proj: nn.Linear, dtype: torch.dtype):
-    """ffn_pack of the block's folded FFN input weight and its output weight (cached like them)."""
+def _ffn_packed(block: nn.Module, proj: nn.Linear, dtype: torch.dtype, w3=None):
+    """ffn_pack of the block's folded FFN input weight and its output weight (cached like them), and
+    with w3 = (tag, source parameters, builder of W3) the next projection's weight appended."""
     lin, out = block.ffn[0], block.ffn[3]
+    tag, src, w3_build = w3 if w3 is not None else ("", (), None)
 
     def build():
         w, _ = _ffn_in_fused(block, proj, dtype)
-        return (ffn_pack(w, out.weight.to(dtype)),)
+        return (ffn_pack(w, out.weight.to(dtype), w3_build().to(dtype) if w3_build else None),)
 
-    return _cached(block, "_ffn_packed", (lin.weight, lin.bias, proj.weight, proj.bias, out.weight), dtype, build)[0]
+    return _cached(block, "_ffn_packed" + tag, (lin.weight, lin.bias, proj.weight, proj.bias, out.weight) + tuple(src), dtype,
+                   build)[0]
+
+
+def _cross_qkv(ca: nn.Module, dtype: torch.dtype):
+    """CrossBlock to_qk | to_v stacked (one projection; lightglue.py:158-166)."""
+    return _cached(ca, "_qkv_stacked", (ca.to_qk.weight, ca.to_qk.bias, ca.to_v.weight, ca.to_v.bias), dtype,
+                   lambda: (torch.cat((ca.to_qk.weight, ca.to_v.weight), 0), torch.cat((ca.to_qk.bias, ca.to_v.bias), 0)))
 
 
 def _qkv_perm(block: nn.Module, dtype: torch.dtype):
@@ -465,9 +511,7 @@ class TransformerLayer(nn.Module):
         c0, c1 = attention(qkv)                                          # self0, self1: one launch
         w0, b0 = _ffn_in_fused(sa, sa.out_proj, x.dtype)
         x = _Hip.ffn(x, c0, c1, w0, b0, sa.ffn[1], sa.ffn[3].weight, sa.ffn[3].bias, _ffn_packed(sa, sa.out_proj, x.dtype))
-        wc, bc = _cached(ca, "_qkv_stacked", (ca.to_qk.weight, ca.to_qk.bias, ca.to_v.weight, ca.to_v.bias),
-                         x.dtype, lambda: (torch.cat((ca.to_qk.weight, ca.to_v.weight), 0),
-                                           torch.cat((ca.to_qk.bias, ca.to_v.bias), 0)))
+        wc, bc = _cross_qkv(ca, x.dtype)
         (qk0, qk1), (v0, v1) = _Hip.linear_split2(x, wc, bc, ca.heads, splits)
         m0, m1 = attention([(qk0, qk1, v1), (qk1, qk0, v0)])            # cross: one launch
         w0, b0 = _ffn_in_fused(ca, ca.to_out, x.dtype)
@@ -493,6 +537,20 @@ class MatchAssignment(nn.Module):
     def hip16_ok(self, x: torch.Tensor, m: int, n: int) -> bool:
         return x.dtype == torch.float16 and x.is_cuda and x.shape[-1] == 256 and n % 8 == 0 and n <= 2048 and m <= 2048
 
+    def aug_weights(self, dtype: torch.dtype, rows: int = 384):
+        """[W_final / scale ; w_match ; 0] [rows, d] and its bias (the head's one projection, cached)."""
+        fp, mt = self.final_proj, self.matchability
+        d = fp.weight.shape[1]
+
+        def build():
+            w = torch.zeros((rows, d), dtype=torch.float32, device=fp.weight.device)
+            b = torch.zeros((rows,), dtype=torch.float32, device=fp.weight.device)
+            w[:d], b[:d] = fp.weight.float() / self.scale, fp.bias.float() / self.scale
+            w[d], b[d] = mt.weight.float()[0], mt.bias.float()[0]
+            return w, b
+
+        return _cached(self, f"_assign_aug{rows}", (fp.weight, fp.bias, mt.weight, mt.bias), dtype, build)
+
     def forward_rows(self, x: torch.Tensor, pr: int, m: int, n: int) -> torch.Tensor:
         """fp16 hip path on both images' rows x [1, P*(m+n), d] at once: ONE projection with
         [W_final / scale ; w_match ; 0], then lg_assign_scores: the similarity of its fp16 halves by
@@ -502,16 +560,7 @@ class MatchAssignment(nn.Module):
         the output equals the reference's fp16(final_proj(d)) / scale except for weights, biases or
         outputs that small, which differ by at most that subnormal rounding."""
         d = x.shape[-1]
-        fp, mt = self.final_proj, self.matchability
-
-        def build():
-            w = torch.zeros((384, d), dtype=torch.float32, device=x.device)
-            b = torch.zeros((384,), dtype=torch.float32, device=x.device)
-            w[:d], b[:d] = fp.weight.float() / self.scale, fp.bias.float() / self.scale
-            w[d], b[d] = mt.weight.float()[0], mt.bias.float()[0]
-            return w, b
-
-        w, b = _cached(self, "_assign_aug", (fp.weight, fp.bias, mt.weight, mt.bias), x.dtype, build)
+        w, b = self.aug_weights(x.dtype, 384)
         v = _Hip.linear(x, w, b).view(pr, m + n, 384)
         return _Hip.assign_scores(v, m, d)   # sim (fp16) and the dual log-softmax: two launches
 
@@ -591,13 +640,85 @@ class LightGlueMatcher(nn.Module):
             cos, sin = cos.reshape(1, rows, -1), sin.reshape(1, rows, -1)  # [1, P*(M+N), 64], broadcast over heads
             if hip:
                 cos, sin = cos.contiguous(), sin.contiguous()
-        for layer in self.transformers:
-            x = layer(x, cos, sin, splits, self.attention, hip)
         head = self.log_assignment[self.n_layers - 1]
-        scores = head.forward_rows(x, pr, m, n) if hip and head.hip16_ok(x, m, n) else None
+        if hip and self.chain_ok(x, m, n):
+            x, scores = self._forward_chain(x, cos, sin, splits)
+        else:
+            for layer in self.transformers:
+                x = layer(x, cos, sin, splits, self.attention, hip)
+            scores = head.forward_rows(x, pr, m, n) if hip and head.hip16_ok(x, m, n) else None
         x = x.view(pr, m + n, x.shape[-1])
         d0, d1 = x[:, :m], x[:, m:]
         return d0, d1, scores if scores is not None else head(d0, d1, hip)
+
+    # Which projections the chained path folds into the FFN launch before them (s: the cross block's
+    # to_qk | to_v, q: the next layer's Wqkv, h: the head's projection). Measured
+    # (profiles/r06/chain_kinds_forward_ab.jsonl, ms per forward, none / s / h / sh / sqh): P = 1 n = 1024
+    # 0.496 / 0.481 / 0.494 / 0.480 / 0.492, P = 4 0.790 / 0.729 / 0.747 / 0.723 / 0.772, P = 16 2.165 /
+    # 2.133 / 2.163 / 2.128 / 2.183: "sh" everywhere; folding Wqkv (768 channels, 384 KiB more per
+    # workgroup's stream) costs the launch more than the separate projection takes. Outputs bitwise
+    # equal in every form. LG_CHAIN (or this attribute) overrides, for A/B.
+    chain_kinds: Optional[str] = None
+
+    def _chain_kinds(self, rows: int) -> str:
+        if self.chain_kinds is not None:
+            return self.chain_kinds
+        return os.environ.get("LG_CHAIN", "sh")
+
+    def chain_ok(self, x: torch.Tensor, m: int, n: int) -> bool:
+        """The chained fp16 path: every block fusable (4 x 64 heads, d = 256) and the fp16 head."""
+        return (self.n_layers > 0 and all(_fused_ok(x, layer.self_attn) for layer in self.transformers) and
+                self.log_assignment[self.n_layers - 1].hip16_ok(x, m, n))
+
+    def _forward_chain(self, x, cos, sin, splits):
+        """fp16 hip path with the layers chained (round 6): FFN launches also project their output for
+        the attention that follows (lg_linear_cat_ffn_proj) — by default the self block's FFN the cross
+        block's to_qk | to_v and the last FFN the assignment head's [W_final / scale ; w_match]
+        (chain_kinds) — so a layer is 5 launches (Wqkv, self attention, FFN + cross projection, cross
+        attention, FFN) and a forward 1 + 5 L + 3 (inputs, the layers, the head's similarity, logsumexp
+        close and combine; lightglue.py:328-353)."""
+        dt = x.dtype
+        m, n, pr = _sp(splits)
+        kinds = self._chain_kinds(x.shape[1])
+        layers = self.transformers
+        head = self.log_assignment[len(layers) - 1]
+        qkv = None
+        for li, layer in enumerate(layers):
+            sa, ca = layer.self_attn, layer.cross_attn
+            if qkv is None:
+                wq, bq = _qkv_perm(sa, dt)
+                qkv = _Hip.linear_qkv_rotary(x, wq, bq, cos, sin, sa.heads, splits)
+            c0, c1 = self.attention(qkv)                                          # self0, self1: one launch
+            _, b0 = _ffn_in_fused(sa, sa.out_proj, dt)
+            wc, bc = _cross_qkv(ca, dt)
+            if "s" in kinds:
+                pk = _ffn_packed(sa, sa.out_proj, dt, ("_x", (ca.to_qk.weight, ca.to_qk.bias, ca.to_v.weight, ca.to_v.bias),
+                                                       lambda ca=ca: _cross_qkv(ca, dt)[0]))
+                x, ((qk0, qk1), (v0, v1)) = _Hip.ffn_proj(x, c0, c1, b0, sa.ffn[1], sa.ffn[3].bias, pk, 1, bc, splits)
+            else:
+                w0, _ = _ffn_in_fused(sa, sa.out_proj, dt)
+                x = _Hip.ffn(x, c0, c1, w0, b0, sa.ffn[1], sa.ffn[3].weight, sa.ffn[3].bias, _ffn_packed(sa, sa.out_proj, dt))
+                (qk0, qk1), (v0, v1) = _Hip.linear_split2(x, wc, bc, ca.heads, splits)
+            m0, m1 = self.attention([(qk0, qk1, v1), (qk1, qk0, v0)])          # cross: one launch
+            w0, b0 = _ffn_in_fused(ca, ca.to_out, dt)
+            qkv = v = None
+            if li + 1 < len(layers) and "q" in kinds:
+                nsa = layers[li + 1].self_attn
+                _, bq = _qkv_perm(nsa, dt)
+                pk = _ffn_packed(ca, ca.to_out, dt, ("_q", (nsa.Wqkv.weight, nsa.Wqkv.bias),
+                                                     lambda nsa=nsa: _qkv_perm(nsa, dt)[0]))
+                x, qkv = _Hip.ffn_proj(x, m0, m1, b0, ca.ffn[1], ca.ffn[3].bias, pk, 2, bq, splits, cos, sin)
+            elif li + 1 == len(layers) and "h" in kinds:
+                _, b3 = head.aug_weights(dt, 512)
+                hp = (head.final_proj.weight, head.final_proj.bias, head.matchability.weight, head.matchability.bias)
+                pk = _ffn_packed(ca, ca.to_out, dt, ("_h", hp, lambda head=head: head.aug_weights(dt, 512)[0]))
+                x, v = _Hip.ffn_proj(x, m0, m1, b0, ca.ffn[1], ca.ffn[3].bias, pk, 3, b3, splits, n_store=384)
+            else:
+                x = _Hip.ffn(x, m0, m1, w0, b0, ca.ffn[1], ca.ffn[3].weight, ca.ffn[3].bias, _ffn_packed(ca, ca.to_out, dt))
+        if v is None:
+            w, b = head.aug_weights(dt, 384)
+            v = _Hip.linear(x, w, b)
+        return x, _Hip.assign_scores(v.view(pr, m + n, 384), m, x.shape[-1])
 
     def match(self, kpts0, kpts1, desc0, desc1):
         """forward + filter_matches (the demo's post-processing); for P > 1 pairs a list of

@@ -427,9 +427,28 @@ def test_ffn_and_form_hooks_validate_before_touching_the_device(lib):
     for bad in (dict(x=None), dict(w2=None), dict(h=None), dict(out=A), dict(out=A + 4), dict(heads=0),
                 dict(heads=3), dict(pairs=-1), dict(eps=-1.0), dict(x=A + 8), dict(wp=A + 8)):
         assert call(**{**bad, "pairs": 0 if "pairs" not in bad else bad["pairs"]}) == 1, bad
-    assert lib.lg_ffn_packed_bytes(4) == (512 * 512 + 256 * 512) * 2 and lib.lg_ffn_packed_bytes(3) == 0
-    for bad in ((A, A, 3, A), (None, A, 4, A), (A, A, 4, None), (A, A + 4, 4, A)):
+    assert lib.lg_ffn_packed_bytes(4, 0) == (512 * 512 + 256 * 512) * 2 and lib.lg_ffn_packed_bytes(3, 0) == 0
+    assert lib.lg_ffn_packed_bytes(4, 768) == (512 * 512 + 256 * 512 + 768 * 256) * 2 and lib.lg_ffn_packed_bytes(4, 384) == 0
+    for bad in ((A, A, None, 0, 3, A), (None, A, None, 0, 4, A), (A, A, None, 0, 4, None), (A, A + 4, None, 0, 4, A),
+                (A, A, None, 512, 4, A), (A, A, A + 8, 768, 4, A), (A, A, A, 256, 4, A)):
         assert lib.lg_ffn_pack(*bad, None) == 1, bad
+    # lg_linear_cat_ffn_proj: kind, the outputs its kind needs, n_store, alignment
+    import ctypes
+    outs = (ctypes.c_void_p * 6)(*([A] * 6))
+
+    def proj(**kw):
+        a = dict(x=A, c0=A, c1=A, heads=4, n0=8, n1=8, pairs=0, b1=A, g=A, be=A, eps=1e-5, b2=A, wp=A, kind=1, b3=A,
+                 cs=A, sn=A, ns=0, outs=outs, out=2 * A)
+        a.update(kw)
+        return lib.lg_linear_cat_ffn_proj(a["x"], a["c0"], a["c1"], a["heads"], a["n0"], a["n1"], a["pairs"], a["b1"],
+                                          a["g"], a["be"], a["eps"], a["b2"], a["wp"], a["kind"], a["b3"], a["cs"],
+                                          a["sn"], a["ns"], a["outs"], a["out"], None)
+
+    assert proj() == 0 and proj(kind=2) == 0 and proj(kind=3, ns=384) == 0
+    for bad in (dict(kind=0), dict(kind=4), dict(heads=2), dict(wp=None), dict(out=A), dict(kind=2, cs=None),
+                dict(kind=3, ns=0), dict(kind=3, ns=12), dict(kind=3, ns=520), dict(b3=None),
+                dict(outs=(ctypes.c_void_p * 6)(A, A, A, None, A, A))):
+        assert proj(**bad) == 1, bad
     prev = lib.lg_linear_set_wide(7)              # clamped to 5
     try:
         assert lib.lg_linear_set_wide(-5) == 5    # clamped to -1

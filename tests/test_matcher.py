@@ -137,6 +137,15 @@ def test_ffn_pack_layout():
     exp1 = w1[(64 * w + 32 * b + r)[..., None], (16 * j1 + 8 * hh)[..., None] + e]
     exp2 = w2[(32 * w + r)[..., None].clamp(max=255), (16 * (i - 64).clamp(min=0) + 8 * hh)[..., None] + e]
     assert torch.equal(got, torch.where((i < 64)[..., None], exp1, exp2))
+    for n3 in (512, 768):  # lg_linear_cat_ffn_proj's W3 after W2: piece 96 + nb3 j + b
+        w3 = torch.arange(n3 * 256, dtype=torch.float32).reshape(n3, 256) + 0.5
+        nb3 = n3 // 256
+        got = matcher.ffn_pack(w1, w2, w3).reshape(8, 96 + 16 * nb3, 64, 8)
+        assert torch.equal(got[:, :96], matcher.ffn_pack(w1, w2).reshape(8, 96, 64, 8))
+        w, i, l = torch.meshgrid(torch.arange(8), torch.arange(16 * nb3), torch.arange(64), indexing="ij")
+        j, b, r, hh = i // nb3, i % nb3, l % 32, l // 32
+        exp3 = w3[(32 * (nb3 * w + b) + r)[..., None], (16 * j + 8 * hh)[..., None] + e]
+        assert torch.equal(got[:, 96:], exp3)
 
 
 def _gpu_run(name, dtype, glue="hip"):
@@ -732,8 +741,8 @@ def test_ffn_rows_kernel(pairs, n0, n1):
         ln.weight.copy_(1 + 0.1 * rnd(512))
         ln.bias.copy_(0.1 * rnd(512))
         wp = mt.ffn_pack(w, w2)
-        packed_c = torch.empty(lib.lg_ffn_packed_bytes(h) // 2, dtype=dt, device=dev)
-        assert lib.lg_ffn_pack(w.data_ptr(), w2.data_ptr(), h, packed_c.data_ptr(), None) == 0
+        packed_c = torch.empty(lib.lg_ffn_packed_bytes(h, 0) // 2, dtype=dt, device=dev)
+        assert lib.lg_ffn_pack(w.data_ptr(), w2.data_ptr(), None, 0, h, packed_c.data_ptr(), None) == 0
         outs = {}
         for mode in (0, 1):
             prev = lib.lg_linear_set_ffn_fused(mode)
@@ -755,6 +764,54 @@ def test_ffn_rows_kernel(pairs, n0, n1):
     assert err_rows <= 2e-2 and err_two <= 2e-2
     assert torch.equal(outs[2], outs[1])  # the default: one launch
     assert torch.equal(no_pack, outs[0]) and torch.equal(packed_c, wp)  # lg_ffn_pack == ffn_pack
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pairs,n0,n1", [(1, 512, 512), (1, 1024, 1024), (1, 700, 1301), (3, 37, 70), (5, 1000, 1011),
+                                         (16, 1024, 1024), (1, 1, 63), (2, 60, 1)])
+def test_ffn_proj_equals_ffn_then_projection(pairs, n0, n1):
+    """lg_linear_cat_ffn_proj (the FFN and, in the same launch, the projection of its output that the next
+    attention needs) against lg_linear_cat_ffn followed by that projection's own call on the FFN's
+    output — lg_linear_split2 (to_qk | to_v), lg_linear_qkv_rotary (Wqkv + rotary), lg_linear (the
+    assignment head's 384 channels of a 512-row W3) — bitwise: the same k-step order and output arithmetic
+    (32 / 64-row workgroups, ragged rows, pairs whose rows cross workgroup and image boundaries)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lightglue_amd import matcher as mt
+
+    dev, dt, h = torch.device("cuda:0"), torch.float16, 4
+    gen = torch.Generator().manual_seed(31 + pairs + n0)
+    rnd = lambda *s: torch.randn(*s, generator=gen).to(dev, dt)  # noqa: E731
+    m = pairs * (n0 + n1)
+    sp = (n0, n1, pairs)
+    with torch.no_grad():
+        x = rnd(1, m, 256) * 0.5
+        c0, c1 = rnd(pairs, h, n0, 64), rnd(pairs, h, n1, 64)
+        w, b = rnd(512, 512) * 0.05, rnd(512) * 0.1
+        w2, b2 = rnd(256, 512) * 0.05, rnd(256) * 0.1
+        ln = torch.nn.LayerNorm(512).to(dev, dt)
+        ln.weight.copy_(1 + 0.1 * rnd(512))
+        ln.bias.copy_(0.1 * rnd(512))
+        ang = rnd(1, m, 32).float()
+        cos = torch.cos(ang).repeat_interleave(2, -1).to(dt).contiguous()
+        sin = torch.sin(ang).repeat_interleave(2, -1).to(dt).contiguous()
+        ref_x = mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2, mt.ffn_pack(w, w2))
+        w3s, b3s = rnd(512, 256) * 0.06, rnd(512) * 0.1
+        w3q, b3q = rnd(768, 256) * 0.06, rnd(768) * 0.1
+        w3h, b3h = rnd(512, 256) * 0.06, rnd(512) * 0.1
+        w3h[384:], b3h[384:] = 0, 0
+        got_s = mt._Hip.ffn_proj(x, c0, c1, b, ln, b2, mt.ffn_pack(w, w2, w3s), 1, b3s, sp)
+        got_q = mt._Hip.ffn_proj(x, c0, c1, b, ln, b2, mt.ffn_pack(w, w2, w3q), 2, b3q, sp, cos, sin)
+        got_h = mt._Hip.ffn_proj(x, c0, c1, b, ln, b2, mt.ffn_pack(w, w2, w3h), 3, b3h, sp, n_store=384)
+        ref_s = mt._Hip.linear_split2(ref_x, w3s, b3s, h, sp)
+        ref_q = mt._Hip.linear_qkv_rotary(ref_x, w3q, b3q, cos, sin, h, sp)
+        ref_h = mt._Hip.linear(ref_x, w3h[:384].contiguous(), b3h[:384].contiguous())
+        torch.cuda.synchronize()
+    for got in (got_s, got_q, got_h):
+        assert torch.equal(got[0], ref_x)
+    flat = lambda o: [t for u in o for t in u]  # noqa: E731
+    for a_, b_ in zip(flat(got_s[1]) + flat(got_q[1]) + [got_h[1]], flat(ref_s) + flat(ref_q) + [ref_h]):
+        assert torch.equal(a_, b_), float((a_.float() - b_.float()).abs().max())
 
 
 @pytest.mark.gpu

@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--ops", default="1x512,1x1024,1x2048,2x1024,4x1024,8x1024")
     ap.add_argument("--forwards", default="1x512,1x1024,1x2048,4x1024")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--chains", default=None, help="A/B of the chained forward's fused projections (LG_CHAIN values, "
+                    "comma-separated, e.g. 'sqh,sh,'): forwards only, against the first")
     a = ap.parse_args()
     modes = [int(m) for m in a.modes.split(",")]
     lib = _lib.load()
@@ -80,6 +82,8 @@ def main():
             del graphs
 
         model = mt.LightGlueMatcher(n_layers=9).eval()
+        if a.chains is not None:
+            return chain_ab(a, model, dev, dt, st)
         model.load_state_dict(mt.seeded_state_dict(7, 9), strict=True)
         model = model.to(dev, dt)
         for P, n in sizes(a.forwards):
@@ -106,6 +110,34 @@ def main():
                               "scores_max_abs_vs_first": {str(m): float((res[m][2] - r0[2]).abs().max()) for m in modes}}),
                   flush=True)
             del graphs
+
+
+def chain_ab(a, model, dev, dt, st):
+    model.load_state_dict(mt.seeded_state_dict(7, 9), strict=True)
+    model = model.to(dev, dt)
+    chains = a.chains.split(",")
+    for P, n in sizes(a.forwards):
+        ps = [mt.synthetic_pair(80 + i, n, n) for i in range(P)]
+        pair = tuple(torch.cat([p[j] for p in ps], 0).to(dev, dt) for j in range(4))
+        graphs, res = {}, {}
+        for c in chains:
+            model.chain_kinds = c
+            with torch.cuda.stream(st):
+                for _ in range(2):
+                    res[c] = model(*pair)
+                st.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=st):
+                    model(*pair)
+            graphs[c] = g
+        model.chain_kinds = None
+        torch.cuda.synchronize()
+        t = replay_ms(graphs, st, 1, rounds=21)
+        r0 = res[chains[0]]
+        print(json.dumps({"forward": f"P={P}", "n": n, "ms": {c: round(t[c], 4) for c in chains},
+                          "same_as_first": {c: all(torch.equal(u, w) for u, w in zip(res[c], r0)) for c in chains}}),
+              flush=True)
+        del graphs
 
 
 if __name__ == "__main__":

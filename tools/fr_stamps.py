@@ -1,7 +1,10 @@
 """Diagnostic: where ffn_rows_kernel's time goes (stamps build, -DLG_FR_STAMPS: per wave, s_memtime
 cycles of chained segments; see csrc/lightglue_linear.hip).
 
-    MHA_HD64_LIB=lib/ab/libmha_hd64_frstamps.so python tools/fr_stamps.py [P=1] [n=1024]
+    MHA_HD64_LIB=lib/ab/libmha_hd64_frstamps.so python tools/fr_stamps.py [P=1] [n=1024] [kind=0]
+
+kind 0: lg_linear_cat_ffn; 1 / 2 / 3: lg_linear_cat_ffn_proj with the split2 / qkv / plain projection
+(segment "phase3": the projection and its epilogue).
 """
 import ctypes
 import json
@@ -20,6 +23,7 @@ from lightglue_amd import matcher as mt  # noqa: E402
 def main():
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 1
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    kind = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     lib = _lib.load()
     fn = lib.lg_diag_fr_stamps
     fn.restype, fn.argtypes = ctypes.c_int32, [ctypes.c_void_p]
@@ -31,13 +35,23 @@ def main():
     c0, c1 = rnd(P, h, n, 64), rnd(P, h, n, 64)
     w, b, w2, b2 = rnd(512, 512) * 0.05, rnd(512) * 0.1, rnd(256, 512) * 0.05, rnd(256) * 0.1
     ln = torch.nn.LayerNorm(512).to(dev, dt)
-    wp = mt.ffn_pack(w, w2)
-    names = ["prologue", "phase1", "layernorm_gelu", "phase2", "epilogue", "total"]
+    n3 = {0: 0, 1: 512, 2: 768, 3: 512}[kind]
+    w3, b3 = (rnd(n3, 256) * 0.06, rnd(n3) * 0.1) if n3 else (None, None)
+    wp = mt.ffn_pack(w, w2, w3)
+    ang = rnd(1, M, 32).float()
+    cs, sn = (torch.cos(ang).repeat_interleave(2, -1).to(dt).contiguous(), torch.sin(ang).repeat_interleave(2, -1).to(dt).contiguous())
+
+    def call():
+        if kind == 0:
+            return mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2, wp)
+        return mt._Hip.ffn_proj(x, c0, c1, b, ln, b2, wp, kind, b3, (n, n, P), cs, sn, 384)
+
+    names = ["prologue", "phase1", "layernorm_gelu", "phase2", "epilogue", "total", "entry", "phase3"]
     wgs = min(256, (M + 31) // 32 if M <= 8192 else (M + 63) // 64)  # (stamps of the first 256)
     rows = []
     for rep in range(6):
         for _ in range(3):  # back to back, as in a forward
-            mt._Hip.ffn(x, c0, c1, w, b, ln, w2, b2, wp)
+            call()
         torch.cuda.synchronize()
         buf = np.zeros(256 * 8 * 8, dtype=np.uint64)
         assert fn(buf.ctypes.data) == 0
@@ -45,8 +59,8 @@ def main():
         if rep:
             rows.append(a)
     a = np.concatenate(rows, 0)
-    out = {"P": P, "n": n, "M": M, "workgroups": wgs,
-           "median_cycles": {k: float(np.median(a[:, :, i])) for i, k in enumerate(names)},
+    out = {"P": P, "n": n, "M": M, "kind": kind, "workgroups": wgs,
+           "median_cycles": {k: float(np.median(a[:, :, i])) for i, k in enumerate(names) if k != "entry"},
            "max_total": float(a[:, :, 5].max()),
            "entry_spread_cycles": float(np.median(a[:, :, 6].max(1) - a[:, :, 6].min(1)))}
     last = rows[-1]
