@@ -232,19 +232,21 @@ struct StreamScores {
     bool rs;        // some query of the wave exceeds the running max by > kRescaleThr (wave-uniform)
 };
 
-// Speculative running max (-DMHA_STREAM_SPEC=1: an A/B build, not shipped; round 5, VERDICT r04
-// item 2's "j2" step): an item's running max is its tile 0's and never moves, so the middle and
-// tail steps carry no row max of the next tile, no rescale decision and no rescale (≈ 20 of the
-// step's ≈ 44 non-exponential vector instructions). Exact while no later score exceeds it by
-// 2^16 (the fp16 P would overflow; below that fp16's relative precision does not depend on
-// magnitude and the row sums and O accumulate in fp32). An overflow makes the row sum +Inf (NaN
-// keys: NaN), which the epilogue sees: the item is marked, and at the end of the kernel the wave
-// recomputes its rows of every marked item with an exact online softmax (exact_item below). Measured
-// (profiles/r05/stream_spec_*): the step 1.04 -> 0.97 us, 32 calls 0.324 -> 0.342 of peak, 64 calls
-// 0.350 -> 0.370 on random inputs — but one key per head that beats tile 0's best by 2^16 (a
-// peaked attention row) sends one item per head down the rare path and the launch from 41 to 134
-// us, where the lazy-rescale form pays 1-4 %. A data-dependent 3x cliff is not a trade the default
-// kernel takes; the lazy form below stays the default.
+// Speculative running max (-DMHA_STREAM_SPEC=1: an A/B build, not shipped): an item's running max is
+// its tile 0's and never moves, so the middle and tail steps carry no row max of the next tile, no
+// rescale decision and no rescale (≈ 20 of the step's ≈ 44 non-exponential vector instructions).
+// Exact while no later score exceeds it by 2^16 (the fp16 P would overflow; below that fp16's
+// relative precision does not depend on magnitude and the row sums and O accumulate in fp32). An
+// overflow makes the row sum +Inf (NaN keys, or the partner row of the row-sum MFMA: NaN), which the
+// epilogue sees: the item is marked, and at the end of the kernel the wave recomputes its rows of
+// every marked item with an exact online softmax (exact_item below) through its own ring slot.
+// Round 6 measurements (profiles/r06/stream_spec_*.jsonl, lazy -> spec): random inputs 32 calls
+// 44.0 -> 41.3 us (tools/spec_rare_cost.py), but bench.py's 32 / 64-call lines 41.4 -> 41.2 and
+// 76.1 -> 75.4 us only; one spike key per head 44.3 -> 70.1 us (gain 3) and 45.0 -> 94.9 (gain 6:
+// secondary overflows mark nearly every item); and the seeded matcher's batched forwards, whose
+// attention rows do overflow (tools/matcher_nan_probe.py), 1.278 -> 1.361 ms at P = 8, 2.333 ->
+// 2.553 at P = 16. A re-run costs a whole item, so no rare path makes a marked fraction f cheaper
+// than ≈ 1 + 1.3 f; the lazy form below stays the default.
 #ifndef MHA_STREAM_SPEC
 #define MHA_STREAM_SPEC 0
 #endif
@@ -419,8 +421,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
     // O = Oᵀ / l of an item (rows past nq: dropped by the descriptor)
     auto epilogue = [&](__amdgpu_buffer_rsrc_t o_rs, int q0, unsigned qbad_it, int ord) {
         if constexpr (MHA_STREAM_SPEC) {
-            unsigned lb;  // (the bits through an asm move: -fno-honor-nans folds a float class test)
-            asm volatile("v_mov_b32 %0, %1" : "=v"(lb) : "v"(l_acc[0]));
+            // the bits behind an empty asm (-fno-honor-nans folds a float class test). Not an asm
+            // v_mov: the flush's epilogue follows the last row-sum MFMA directly, and the hazard
+            // recognizer puts no wait states before an instruction inside inline asm — such a move
+            // read the register before the MFMA had written it (an overflow missed, its rows left
+            // NaN; tools/check_mfma_hazards.py audits the library for it)
+            unsigned lb = __builtin_bit_cast(unsigned, l_acc[0]);
+            asm volatile("" : "+v"(lb));
             const bool over = (lb & 0x7f800000u) == 0x7f800000u && !((qbad_it >> r) & 1u);
             if (__builtin_amdgcn_ballot_w64(over) != 0) dirty |= 1ull << (ord < 63 ? ord : 63);
         }
@@ -776,14 +783,28 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         const bool more = j + G < je;
         nxt = stream_item<MULTI, OSZ, NW>(a, more ? j + G : j, more);
     }
-    // SPEC's rare path: this wave's 32 rows of item jj, exactly — a running max per 64-key tile
-    // (exact online softmax, rescale at every move), the step's MFMA forms with their operands
-    // loaded from global memory: K fragments as read_k reads the ring (key row r / r + 32, chunk
-    // 2s + hh), Vᵀ fragments element by element (lane (dim, k-group g) holds V[key][dim] for the 8
-    // keys that P's pack (jj, ss) puts at k = 8g .. 8g + 7), then the item's epilogue.
+    // SPEC's rare path: this wave's 32 rows of item jj, exactly — a running max per 64-key tile (exact
+    // online softmax, rescale at every move) on the step's MFMA forms and fragment reads. Runs after
+    // the workgroup's last barrier, when the ring is idle: the wave streams each K / V tile by LDS-DMA
+    // into ring slot `wave` (its own: 16 KiB, the main loop's image layout and swizzles) and reads
+    // the fragments as the steps do (read_k, read_v: ds_read_b128 / ds_read_b64_tr_b16); the next
+    // tile's DMA is issued once the current one's fragments are in registers, so it lands under the
+    // current tile's arithmetic. (Round 5's form loaded K fragments with 16-B and Vᵀ with 2-byte
+    // global loads, one item ~90 us; profiles/r05/stream_spec_rare_cost.jsonl.)
+    const unsigned xs_base = (unsigned)wave * (unsigned)kSSlot;
+    const unsigned xs_m0 = (unsigned)__builtin_amdgcn_readfirstlane(lds0 + xs_base);
     auto exact_item = [&](int jj) {
         const StreamItem it = stream_item<MULTI, OSZ, NW>(a, jj, true);
         const StreamLoader kv = stream_kv<MULTI>(a, jj, true);
+        auto load_tile = [&](int t) {  // pieces p = rows 8p..8p+7 of K and V (swizzles as issue_tile)
+            const unsigned so = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(t * kTileBytes));
+#pragma unroll
+            for (int pc = 0; pc < 8; ++pc) {
+                lds_dma16(xs_m0 + (unsigned)(pc * 1024), dma_kq(pc & 1), kv.k, so + (unsigned)(pc * 1024));
+                lds_dma16(xs_m0 + (unsigned)(kTileBytes + pc * 1024), dma_v, kv.v, so + (unsigned)(pc * 1024));
+            }
+        };
+        load_tile(0);
         const unsigned qrow = (unsigned)(it.q0 + 32 * wave + r);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
@@ -795,18 +816,20 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
         o1 = f32x16{};
         const int ntl = (it.nkv + kTileKV - 1) / kTileKV;
         for (int t = 0; t < ntl; ++t) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t landed (this wave's own DMA)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) read_k(xs_base, s);
+            read_v(xs_base, 0);
+            read_v(xs_base, 1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // fragments in registers: the slot is free
+            if (t + 1 < ntl) load_tile(t + 1);
             const unsigned kt = (unsigned)(t * kTileKV);
             StreamScores sc;
             const f32x16 zero = {};
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-#pragma unroll
-                for (int kb = 0; kb < 2; ++kb) {
-                    const f16x8 kfr = __builtin_bit_cast(
-                        f16x8, __builtin_amdgcn_raw_buffer_load_b128(kv.k, (kt + (unsigned)(32 * kb + r)) * 128u + (unsigned)(2 * s + hh) * 16u, 0, 0));
-                    f32x16& acc = kb ? sc.s1 : sc.s0;
-                    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kfr, qf[s], s == 0 ? zero : acc, 0, 0, 0);
-                }
+                sc.s0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s], qf[s], s == 0 ? zero : sc.s0, 0, 0, 0);
+                sc.s1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[2 * s + 1], qf[s], s == 0 ? zero : sc.s1, 0, 0, 0);
             }
             if (it.nkv - (int)kt < kTileKV) mask_tile(sc, it.nkv - (int)kt);
             const float mn = fmaxf(m, xhalf_max(tree_max(sc.s0, sc.s1)));
@@ -828,17 +851,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
 #pragma unroll
                 for (int ps = 0; ps < 2; ++ps) {
                     const f32x16& x = pj ? sc.s1 : sc.s0;
-                    f16x8 pk, va, vb;
+                    f16x8 pk;
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        pk[e] = (f16)x[8 * ps + e];
-                        const int i = 8 * ps + e;
-                        const unsigned key = kt + (unsigned)((i & 3) + 8 * (i >> 2) + 4 * hh + 32 * pj);
-                        va[e] = __builtin_bit_cast(f16, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(kv.v, key * 128u + (unsigned)r * 2u, 0, 0));
-                        vb[e] = __builtin_bit_cast(f16, (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(kv.v, key * 128u + (unsigned)(32 + r) * 2u, 0, 0));
-                    }
-                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pk, o0, 0, 0, 0);
-                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vb, pk, o1, 0, 0, 0);
+                    for (int e = 0; e < 8; ++e) pk[e] = (f16)x[8 * ps + e];
+                    o0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfa[pj][ps], pk, o0, 0, 0, 0);
+                    o1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(vfb[pj][ps], pk, o1, 0, 0, 0);
                 }
         }
         l_acc = f32x4{l, l, l, l};
@@ -861,6 +878,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void mha_hd64_stream_kern
     // drain: the loader's trailing (empty) pieces and the output stores
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (MHA_STREAM_SPEC) {
+        // every wave is done with the ring (its flush read the last V image): slot w is wave w's
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+#ifdef MHA_STREAM_RARE_ALL  // diagnostic: every item down the rare path
+        dirty = ~0ull;
+#endif
+#ifdef MHA_STREAM_RARE_NONE  // diagnostic: the speculative output as it is
+        dirty = 0;
+#endif
         if (dirty) {  // (wave-uniform, rare) the exact rows of the marked items, over their stores
             asm volatile("" ::: "memory");
             const int j_first = jb + loc;

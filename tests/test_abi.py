@@ -2,6 +2,7 @@
 include/mha_hd64.h declares, and the plugin's host-side contract mirrors the reference
 (lightglue_attention_plugin/lightglue_attention_plugin.cpp:28-422)."""
 import ctypes
+import importlib.util
 import os
 import re
 import shutil
@@ -409,6 +410,41 @@ def test_built_library_dma_wait_states():
                        text=True, timeout=300)
     m = re.search(r"checked (\d+) LDS-DMA loads; (\d+) wait-state", r.stdout)
     assert r.returncode == 0 and m and int(m.group(1)) > 1000 and int(m.group(2)) == 0, r.stdout[-2000:]
+
+
+def test_mfma_hazard_audit_flags_an_early_read():
+    """tools/check_mfma_hazards.py: a VALU read of an MFMA destination needs the form's wait states
+    (gfx950 16x16x32 f16: 4 passes, 7); MFMAs and s_nop count toward them; a read of other
+    registers is not a hazard."""
+    spec = importlib.util.spec_from_file_location("check_mfma_hazards", os.path.join(REPO, "tools", "check_mfma_hazards.py"))
+    c = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(c)
+    k = "kern"
+
+    def seq(*body):
+        return [(k, mn, ops, 4 * i) for i, (mn, ops) in enumerate(body)]
+
+    mfma = ("v_mfma_f32_16x16x32_f16", "v[32:35], v[128:131], v[156:159], v[32:35]")
+    assert len(c.audit(seq(mfma, ("v_mov_b32_e32", "v33, v32")), set())) == 1       # round 6's flush
+    assert len(c.audit(seq(mfma, ("s_nop", "5"), ("v_mov_b32_e32", "v33, v32")), set())) == 1
+    assert c.audit(seq(mfma, ("s_nop", "6"), ("v_mov_b32_e32", "v33, v32")), set()) == []
+    assert c.audit(seq(mfma, ("v_mfma_f32_32x32x16_f16", "v[0:15], v[1:4], v[5:8], v[0:15]"),
+                       ("v_mov_b32_e32", "v33, v32")), set()) == []
+    assert c.audit(seq(mfma, ("v_mov_b32_e32", "v40, v41")), set()) == []
+
+
+def test_built_library_mfma_result_wait_states():
+    """No VALU instruction of the built gfx950 code objects reads or overwrites an MFMA result
+    sooner than the form's wait states (inline asm on an accumulator gets none from the compiler:
+    round 6's missed overflow in the streaming kernel's flush)."""
+    import shutil
+
+    if not shutil.which("objcopy") or not os.path.exists(os.path.join("/opt/rocm", "lib", "llvm", "bin", "llvm-objdump")):
+        pytest.skip("needs objcopy and the ROCm llvm-objdump")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "check_mfma_hazards.py")], capture_output=True,
+                       text=True, timeout=600)
+    m = re.search(r"checked (\d+) VALU instructions; (\d+) MFMA-result", r.stdout)
+    assert r.returncode == 0 and m and int(m.group(1)) > 100000 and int(m.group(2)) == 0, r.stdout[-3000:]
 
 
 def test_ffn_and_form_hooks_validate_before_touching_the_device(lib):

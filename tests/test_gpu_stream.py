@@ -126,6 +126,67 @@ def test_stream_kernel_running_max_moves(waves, dev, oracle_mod):
 
 
 @pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("nkv", [200, 1100, 2048])
+def test_stream_kernel_every_item_recomputed(nkv, waves, dev, oracle_mod):
+    """The speculative running max's rare path on every item: each 128-row block of every head has
+    one query row whose spike key (gain 8, past tile 0) beats tile 0's max by far more than 2^16, so
+    every item's row sum overflows, every item is marked and every wave re-runs its rows of all of
+    them through its own ring slot after the workgroup's last barrier (csrc/mha_hd64_stream.hip,
+    exact_item). nkv 200 and 1100: a partial last tile; batch 40: 2-3 items per workgroup,
+    so the re-runs follow each other through the same slot. Every row of three heads is checked.
+    Both output types take the 1e-2 contract: on these peaked rows fp16 P's rounding alone puts the
+    fp32 output 6.1e-3 from the fp64 oracle, in the lazy-rescale form (no rare path) as in this one
+    (profiles/r06/stream_rare_path_errors.jsonl, tools/rare_path_errors.py)."""
+    from lightglue_amd import _lib, synth
+
+    lib = _lib.load()
+    batch, nq = 40, 512
+    qn, kn, vn = synth.qkv(4242 + nkv, nq, nkv, batch=batch)
+    for blk in range(nq // 128):
+        kn = synth.spike(qn, kn, 128 * blk + 9 + 11 * blk, 64 + 37 * blk, 8.0)
+    q16, k16, v16 = (synth.round_f16(x) for x in (qn, kn, vn))
+    bsel = [0, 23, batch - 1]
+    ref = oracle_mod.attention_c(q16[bsel], k16[bsel], v16[bsel])
+    q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+    for out_dt in (torch.float16, torch.float32):
+        o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
+        _launch(lib, q, k, v, o, waves=waves)
+        torch.cuda.synchronize()
+        got = o.float().cpu().numpy()
+        assert np.isfinite(got).all()
+        d = _maxdiff(got[bsel], ref)
+        assert d <= TOL, (nkv, waves, out_dt, d)
+
+
+@pytest.mark.parametrize("waves", [4, 8])
+def test_stream_kernel_matcher_overflow_head(waves, dev, oracle_mod):
+    """A head of the seeded fp16 matcher (P = 8 pairs, n = 1024; the layer-7 self-attention launch,
+    tools/matcher_nan_probe.py) whose rows 131, 361 and 816 beat their tile-0 max by just past 2^16:
+    the speculative max overflows there and, through the row-sum MFMA, in the partner rows 147, 377
+    and 800. The overflow of an item whose epilogue is the flush's (the workgroup's last item) was
+    missed until round 6: the check read the row sums with an inline-asm move that the compiler gave
+    no MFMA wait states. Every row against the fp64 oracle (tests/golden/stream_spec_overflow_head.npz)."""
+    import os
+
+    from conftest import REPO
+    from lightglue_amd import _lib
+
+    lib = _lib.load()
+    d = np.load(os.path.join(REPO, "tests", "golden", "stream_spec_overflow_head.npz"))
+    q16, k16, v16 = (d[n].astype(np.float32) for n in "qkv")
+    ref = oracle_mod.attention_c(q16, k16, v16)
+    q, k, v = (_t(x, dev, torch.float16) for x in (q16, k16, v16))
+    for out_dt, tol in ((torch.float16, TOL), (torch.float32, TOL_F32OUT)):
+        o = torch.full(q.shape, float("nan"), dtype=out_dt, device=dev)
+        _launch(lib, q, k, v, o, waves=waves)
+        torch.cuda.synchronize()
+        got = o.float().cpu().numpy()
+        assert np.isfinite(got).all(), np.nonzero(~np.isfinite(got).all(-1))
+        d_ = _maxdiff(got, ref)
+        assert d_ <= tol, (waves, out_dt, d_)
+
+
+@pytest.mark.parametrize("waves", [4, 8])
 def test_stream_kernel_large_negative_logits(waves, dev, oracle_mod):
     """Scores far below zero everywhere (~ -200 raw, as test_gpu_parity.py's case) in a launch of
     several items per workgroup: each item's first tile must set its max (no underflow to l = 0).

@@ -3,7 +3,7 @@
 # failure (no GPU step runs after a fault, abort or timeout). Logs in gpurun_out/<tag>/.
 #   bash tools/gpu/session.sh <tag> <step> [<step> ...]
 # steps: tests[:<pytest -k expr>]  gpu  ffn_ab[:<args>]  bench[:<args>]  smoke  prof_fwd:<P>x<n>
-#        pmc_ffn:<P>:<n>:<mode>
+#        pmc_ffn:<P>:<n>:<mode>  "tool:<tools/NAME.py> [args...]" (one quoted word)
 set -o pipefail
 tag=$1; shift
 O=$PWD/gpurun_out/$tag; mkdir -p "$O"
@@ -24,6 +24,9 @@ for step in "$@"; do
         gpu)    run 1100 gpu_suite.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit $? ;;
         ffn_ab) run 600 "ffn_ab.log" python -u tools/ffn_ab.py $arg || exit $? ;;
         bench)  run 900 "bench.log" python -u bench.py $arg || exit $? ;;
+        tool)   # one diagnostic script of tools/ (its stdout in <name>.log)
+            read -r -a ta <<< "$arg"; tn=${ta[0]}; sfx=$(basename -a "${ta[@]:1}" 2>/dev/null | tr -c 'a-zA-Z0-9\n' '_' | tr '\n' '_')
+            run 600 "${tn}_${sfx:0:60}.log" python -u "tools/${tn}.py" "${ta[@]:1}" || exit $? ;;
         smoke)  run 300 smoke.log python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
         prof_fwd)  # kernel trace of P x n forwards (graph replays), then one forward's timeline
             P=${arg%x*}; n=${arg#*x}; R=$PWD
