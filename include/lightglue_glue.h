@@ -18,7 +18,8 @@
  * header links against the same symbol names and would pass shifted arguments: check
  * lg_glue_abi_version() == LG_GLUE_ABI_VERSION once at load.
  * ABI version 3 (round 6): lg_linear_cat_ffn takes the packed weight stream of its one-launch form
- * (w_packed, after b2; lg_ffn_pack).
+ * (w_packed, after b2; lg_ffn_pack). ABI version 4: lg_ffn_pack writes two layouts (the 16-row
+ * kernel's after the 32-row kernel's; lg_ffn_packed_bytes doubled).
  */
 #ifndef LIGHTGLUE_GLUE_H_
 #define LIGHTGLUE_GLUE_H_
@@ -32,7 +33,7 @@
 extern "C" {
 #endif
 
-#define LG_GLUE_ABI_VERSION 3
+#define LG_GLUE_ABI_VERSION 4
 /* The ABI version of the argument lists below that this library implements. */
 int32_t lg_glue_abi_version(void);
 
@@ -93,9 +94,10 @@ int32_t lg_linear_cat_ln_gelu(const void* x, const void* ctx0, const void* ctx1,
 /* lg_linear_cat_ffn:    the whole FFN with the block's residual (lightglue.py:101-106, 150-151 / 174-175):
  *                       out [n0+n1, d] = x + fp16(W2 · GELU(LayerNorm(W1 · [x | merge_heads(ctx0, ctx1)] + b1)) + b2)
  *                       with d = heads*64 = 256, W1 [2d, 2d], W2 [d, 2d]. With w_packed (W1 and W2 as
- *                       lg_ffn_pack lays them out): ONE launch, whole rows per workgroup (ffn_rows_kernel:
- *                       32 rows up to 8,192, 64 beyond; each wave streams its own weight fragments into
- *                       registers, the GELU output stays in LDS; within 2 fp16 ulps of the two calls).
+ *                       lg_ffn_pack lays them out): ONE launch, whole rows per workgroup (16 rows up to
+ *                       4,096 rows, ffn_rows16_kernel; 32 up to 8,192 and 64 beyond, ffn_rows_kernel; each
+ *                       wave streams its own weight fragments into registers, the GELU output stays in
+ *                       LDS; within 2 fp16 ulps of the two calls).
  *                       With w_packed NULL: lg_linear_cat_ln_gelu into h [m, 2d] then lg_linear(h, W2, b2,
  *                       res = x). h must hold m*2d fp16 either way (unused by the one-launch form); out
  *                       must not alias x (16-B aligned pointers). */
@@ -104,19 +106,24 @@ int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int
                           const void* w2, const void* b2, const void* w_packed, void* h, void* out, hipStream_t stream);
 /* lg_ffn_pack:          W1 [2d, 2d] and W2 [d, 2d] (nn.Linear layout, fp16, d = heads*64 = 256), and for
  *                       lg_linear_cat_ffn_proj a W3 [n3, d] (n3 = 512 or 768; 0: none), re-laid as the
- *                       one-launch FFN reads them: 8 wave streams of (96 + n3/16) KiB, stream w = W1 rows
- *                       64w..64w+63 then W2 rows 32w..32w+31 then W3 rows (n3/8)w.., in 1-KiB pieces i
- *                       (W1: step j, block b at i = 2j + b; W2: step j at i = 64 + j; W3: step j, block b at
- *                       i = 96 + (n3/256) j + b) whose 16-B lane l holds W[row0 + 32b + (l % 32)][16j + 8(l / 32)
- *                       .. + 8] — every load of the kernel one contiguous KiB. lg_ffn_packed_bytes(heads, n3):
- *                       its size (786,432 B for n3 = 0; 0 if heads != 4 or n3 is not 0 / 512 / 768).
+ *                       one-launch FFN reads them, twice. The 32-row kernel's layout: 8 wave streams of
+ *                       (96 + n3/16) KiB, stream w = W1 rows 64w..64w+63 then W2 rows 32w..32w+31 then W3
+ *                       rows (n3/8)w.., in 1-KiB pieces i (W1: step j, block b at i = 2j + b; W2: step j at
+ *                       i = 64 + j; W3: step j, block b at i = 96 + (n3/256) j + b) whose 16-B lane l holds
+ *                       W[row0 + 32b + (l % 32)][16j + 8(l / 32) .. + 8]; then the 16-row kernel's: the same
+ *                       rows per stream in 16-row blocks and k32 steps (W1: i = 4j + b, W2: i = 64 + 2j + b,
+ *                       W3: i = 96 + (n3/128) j + b), lane l = W[row0 + 16b + (l % 16)][32j + 8(l / 16) .. + 8]
+ *                       — every load of either kernel one contiguous KiB. lg_ffn_packed_bytes(heads, n3):
+ *                       the size of both (1,572,864 B for n3 = 0; 0 if heads != 4 or n3 is not 0 / 512 /
+ *                       768).
  *                       Weights are static: pack once per weight update. lg_linear_cat_ffn takes an n3 = 0 pack. */
 size_t lg_ffn_packed_bytes(int32_t heads, int32_t n3);
 int32_t lg_ffn_pack(const void* w1, const void* w2, const void* w3, int32_t n3, int32_t heads, void* packed,
                     hipStream_t stream);
 /* lg_linear_cat_ffn_proj: lg_linear_cat_ffn's one-launch form, then — in the same launch, on its output
- *                       out = x' still in LDS — the projection the next attention needs (bitwise the
- *                       separate call's outputs; round 6):
+ *                       out = x' still in LDS — the projection the next attention needs (the 32/64-row
+ *                       forms bitwise the separate call's outputs; the 16-row form sums each k32 step in
+ *                       one MFMA, within 1 fp16 ulp of them; round 6):
  *                         kind LG_PROJ_SPLIT2: W3 = [W_qk; W_v] [512, d], b3 [512] -> a0, a1, b0, b1 as
  *                                              lg_linear_split2 (outs3[0..3]);
  *                         kind LG_PROJ_QKV:    W3 = Wqkv permuted [768, d], b3 [768], cos / sin [m, 64] ->
@@ -198,9 +205,13 @@ int32_t lg_linear_set_wide(int32_t mode);
  * round of its tiles on, 0 always two launches, 2 always one launch (A/B). The forms agree within fp16
  * rounding, not in every bit (the one-launch variance is two-pass). Returns the previous setting. */
 int32_t lg_linear_set_ln_fused(int32_t on);
-/* Test and benchmark hook for lg_linear_cat_ffn's forms: 1 (the default) the one-launch form when
- * w_packed is given, 0 always the two calls. Returns the previous setting. */
-int32_t lg_linear_set_ffn_fused(int32_t on);
+/* Test and benchmark hook for lg_linear_cat_ffn's (and lg_linear_cat_ffn_proj's) forms: 1 (the
+ * default) the one-launch form when w_packed is given, its kernel by size (16-row tiles up to 4,096
+ * rows, then 32-row up to 8,192, then 64-row); 2 the 32/64-row kernel at every size, 3 the 16-row
+ * kernel at every size (A/B); 0 always the two calls (lg_linear_cat_ffn; lg_linear_cat_ffn_proj has
+ * only the one-launch form and takes 0 as 1). Values outside 0..3 select 1. Returns the previous
+ * setting. */
+int32_t lg_linear_set_ffn_fused(int32_t mode);
 
 #ifdef __cplusplus
 }

@@ -1264,20 +1264,290 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
 #endif
 }
 
+// ---- the 16-row form (round 6): the same FFN (+ phase 3) with v_mfma_f32_16x16x32_f16 on 16-row tiles ----
+// At a few thousand rows the 32-row kernel above fills a quarter of the chip (2,048 rows: 64
+// workgroups) and its time is the per-CU weight stream (each workgroup reads all of W1, W2, W3) plus
+// the LayerNorm+GELU vector work of its 32 x 512 values (~8 k cycles, profiles/r06/ffn_rows_stamps*):
+// 16-row tiles double the workgroups and halve the vector work per CU at the same stream. Operands
+// (cdna_hip_programming.md §3): lane l holds A[i = l & 15][k = 8 (l >> 4) + e] (weights: channel i of a
+// 16-channel block), B[k][j = l & 15] (activation row j), D[4 (l >> 4) + t][l & 15] — channels
+// 4 q + t (q = l >> 4) of row l & 15. The weight stream is lg_ffn_pack's second layout: wave w's
+// pieces are phase 1 W1[64 w + 16 b + i][32 s + 8 q ..] (piece 4 s + b), phase 2 W2[32 w + 16 b + i]
+// (64 + 2 s + b), phase 3 W3[16 (2 NB3 w + b) + i][32 s + 8 q ..] (96 + 2 NB3 s + b): the same channel
+// sets per wave as the 32-row layout, so the rounding and order of every sum are unchanged but for
+// the k order inside an MFMA.
+template <int D, int E3, int NB3>
+__global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16* __restrict__ gamma,
+                                                            const f16* __restrict__ beta, float eps,
+                                                            const f16* __restrict__ wp, const f16* __restrict__ b2,
+                                                            Proj3 q3) {
+    constexpr int MT = 16, K = 512, NO = kFfnOut;
+    constexpr int NP = 96 + NB3 * 16;              // the wave's stream: pieces of 1 KiB
+    constexpr int R = 2 * D;                       // pieces in flight (a register ring)
+    constexpr int NB = 2 * NB3;                    // phase 3: 16-channel blocks per wave
+    constexpr int U3 = 32 * NB3;                   // phase 3: 16-B units per output row
+    constexpr int kA = 0;                          // A tile [16][1 KiB]: x units 0..31, heads 32..63
+    constexpr int kH = kA + MT * 1024;             // h tile [16][1 KiB]
+    constexpr int kX = kH + MT * 1024;             // out / x' tile [16][512 B]
+    constexpr int kS3 = kX + MT * 512;             // phase 3's staging [16][U3 units]
+    constexpr int kPar = kS3 + MT * U3 * 16;       // b1, gamma, beta [512], b2 [256] fp16
+    constexpr int kRed = kPar + (3 * K + NO) * 2;  // row partials [2][16][8 waves] fp32
+    constexpr int kB3 = kRed + 2 * MT * 8 * 4;     // b3 [n3] fp16
+    constexpr int kCS = kB3 + NB3 * 256 * 2;       // E3_QKV: cos / sin rows [2][16][64] fp16
+    constexpr int kEnd = kCS + (E3 == E3_QKV ? 2 * MT * kD * 2 : 0);
+    static_assert(D >= 1 && D <= 16 && (E3 == E3_NONE) == (NB3 == 0) && kEnd <= 160 * 1024, "shape");
+    __shared__ __attribute__((aligned(16))) char smem[kEnd];
+    lds_char* const lds = (lds_char*)smem;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, q = lane >> 4;
+    const int m0 = blockIdx.x * MT;
+    auto tile_unit = [](int row, int u) { return row * 1024 + ((u ^ (row & 15)) << 4); };  // A / h tiles
+    auto x_unit = [](int row, int u) { return row * 512 + ((u ^ (row & 15)) << 4); };      // x' tile
+
+    // ---- A tile (two 16-B units a thread: row f / 64, unit f % 64), the vectors; rows past m repeat
+    // row m - 1 ----
+    f16x8 av[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int f = 512 * i + tid, row = f >> 6, u = f & 63;
+        const int grow = min(m0 + row, p.m - 1);
+        const f16* src;
+        if (u < 32) {
+            src = p.a + (size_t)grow * (K / 2) + u * 8;
+        } else {
+            const LinRow lr = lin_row(p, grow, (u - 32) >> 3);
+            src = (lr.first ? p.ctx0 : p.ctx1) + lr.off + ((u - 32) & 7) * 8;
+        }
+        av[i] = *reinterpret_cast<const f16x8*>(src);
+    }
+    f16x8 pv = {};
+    if (tid < 224) {
+        const f16* const pvs = tid < 64 ? p.bias : tid < 128 ? gamma : tid < 192 ? beta : b2;
+        pv = *reinterpret_cast<const f16x8*>(pvs + (tid & 63) * 8);
+    }
+    constexpr int NVB = NB3 * 256 * 2 / 16;                         // b3 units
+    constexpr int NV3 = NVB + (E3 == E3_QKV ? 2 * MT * 8 : 0);      // + cos / sin units
+    static_assert(NV3 <= 512, "phase 3 vectors");
+    f16x8 v3 = {};
+    if (tid < NV3) {
+        if (tid < NVB) {
+            v3 = *reinterpret_cast<const f16x8*>(q3.b3 + tid * 8);
+        } else {  // table t, row rw (clamped), unit cu % 8
+            const int cu = tid - NVB, t = cu / (MT * 8), rw = min(m0 + (cu % (MT * 8)) / 8, p.m - 1);
+            v3 = *reinterpret_cast<const f16x8*>((t ? q3.sinv : q3.cosv) + (size_t)rw * kD + (cu % 8) * 8);
+        }
+    }
+    asm volatile("s_barrier" ::: "memory");  // (every wave's A loads ahead of the weight stream)
+
+    const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(wp), (short)0, 8 * NP * 1024, 0x00020000);
+    const unsigned wo = (unsigned)(wave * NP * 1024 + lane * 16);
+    auto piece = [&](int i) { return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, wo, i * 1024, 0)); };
+    f16x8 w_[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        w_[i] = piece(i);
+        if (i & 1) __builtin_amdgcn_sched_barrier(0);
+    }
+    auto take = [&](int i) {
+        const f16x8 w = w_[i % R];
+        if (i + R < NP) w_[i % R] = piece(i + R);
+        return w;
+    };
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int f = 512 * i + tid;
+        *(lds_f16x8*)(lds + kA + tile_unit(f >> 6, f & 63)) = av[i];
+    }
+    if (tid < 224) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
+    if (tid < NV3) *(lds_f16x8*)(lds + kB3 + tid * 16) = v3;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+
+    // ---- phase 1: hᵀ (the wave's 64 channels x 16 rows) = W1 · Aᵀ, k32 steps, B read a step ahead ----
+    f32x4 acc[4] = {};
+    f16x8 bf = *(lds_f16x8*)(lds + kA + tile_unit(r, q));
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        f16x8 w4[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) w4[b] = take(4 * s + b);
+        const f16x8 bn = s + 1 < 16 ? *(lds_f16x8*)(lds + kA + tile_unit(r, 4 * (s + 1) + q)) : bf;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w4[b], bf, acc[b], 0, 0, 0);
+        bf = bn;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // ---- LayerNorm: lane (r, q) holds channels 64 w + 16 b + 4 q + t of row r; h = fp16(acc + b1) in
+    // one rounding, the row's sum and sum of squares over the 4 q lanes, then the 8 waves via LDS ----
+    float* const red = (float*)(void*)(smem + kRed);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const u32x2 b4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + (64 * wave + 16 * b + 4 * q) * 2);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float h = (t & 1) ? mixh<1>(acc[b][t], b4[t >> 1]) : mixh<0>(acc[b][t], b4[t >> 1]);
+            acc[b][t] = h;
+            s1 += h;
+            s2 = __builtin_fmaf(h, h, s2);
+        }
+    }
+    s1 += __shfl_xor(s1, 16, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (q == 0) {
+        red[r * 8 + wave] = s1;
+        red[MT * 8 + r * 8 + wave] = s2;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    auto row_sum = [&](int off, int row) {  // the 8 waves' partials of a row, in a fixed order
+        const f32x4 a = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (off + row * 8) * 4);
+        const f32x4 c = *(__attribute__((address_space(3))) f32x4*)(lds + kRed + (off + row * 8 + 4) * 4);
+        return ((a[0] + a[1]) + (a[2] + a[3])) + ((c[0] + c[1]) + (c[2] + c[3]));
+    };
+    {
+        const float mean = row_sum(0, r) * (1.f / K);
+        const float rstd = __builtin_amdgcn_rsqf(fmaxf(row_sum(MT * 8, r) * (1.f / K) - mean * mean, 0.f) + eps);
+        const float nmr = -mean * rstd;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int n = 64 * wave + 16 * b + 4 * q;
+            const u32x2 g4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + K * 2 + n * 2);
+            const u32x2 be4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + 2 * K * 2 + n * 2);
+            f16x4 o;
+#pragma unroll
+            for (int u = 0; u < 4; u += 2) {
+                const f32x2 xr = f32x2{acc[b][u], acc[b][u + 1]} * rstd + nmr;
+                const f32x2 gl = gelu_as2(f32x2{mixf<0>(xr[0], g4[u >> 1], be4[u >> 1]), mixf<1>(xr[1], g4[u >> 1], be4[u >> 1])});
+                o[u] = (f16)gl[0];
+                o[u + 1] = (f16)gl[1];
+            }
+            *(__attribute__((address_space(3))) f16x4*)(lds + kH + tile_unit(r, n >> 3) + 8 * (q & 1)) = o;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // h complete
+
+    // ---- phase 2: outᵀ (the wave's 32 channels x 16 rows) = W2 · hᵀ ----
+    f32x4 o2[2] = {};
+    f16x8 hf = *(lds_f16x8*)(lds + kH + tile_unit(r, q));
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const f16x8 wa = take(64 + 2 * s), wb = take(64 + 2 * s + 1);
+        const f16x8 hn = s + 1 < 16 ? *(lds_f16x8*)(lds + kH + tile_unit(r, 4 * (s + 1) + q)) : hf;
+        o2[0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa, hf, o2[0], 0, 0, 0);
+        o2[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wb, hf, o2[1], 0, 0, 0);
+        hf = hn;
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // ---- out = fp16(fp16(acc + b2) + x): fp16(acc + b2) into the x' tile, then one 16-B unit a thread
+    // (row tid / 32, unit tid % 32) with x from the A tile, to memory and back into the x' tile ----
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const int c = 32 * wave + 16 * b + 4 * q;
+        const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kPar + 3 * K * 2 + c * 2);
+        const f16x4 v = f16x4{lin_val(o2[b][0], b4[0]), lin_val(o2[b][1], b4[1]), lin_val(o2[b][2], b4[2]),
+                              lin_val(o2[b][3], b4[3])};
+        *(__attribute__((address_space(3))) f16x4*)(lds + kX + x_unit(r, c >> 3) + 8 * (q & 1)) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    {
+        const int row = tid >> 5, u = tid & 31;
+        f16x8 v = *(lds_f16x8*)(lds + kX + x_unit(row, u));
+        const f16x8 xr = *(lds_f16x8*)(lds + kA + tile_unit(row, u));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], xr[e]);
+        if (m0 + row < p.m) *reinterpret_cast<f16x8*>(p.out[0] + (size_t)(m0 + row) * NO + 8 * u) = v;
+        if constexpr (E3 != E3_NONE) *(lds_f16x8*)(lds + kX + x_unit(row, u)) = v;
+    }
+    if constexpr (E3 != E3_NONE) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // x' complete
+        // ---- phase 3: the wave's NB blocks of 16 output channels, c = 16 (NB w + b) + 4 q + t ----
+        f32x4 a3[NB] = {};
+        f16x8 xf = *(lds_f16x8*)(lds + kX + x_unit(r, q));
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            f16x8 w3[NB];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) w3[b] = take(96 + NB * s + b);
+            const f16x8 xn = s + 1 < 8 ? *(lds_f16x8*)(lds + kX + x_unit(r, 4 * (s + 1) + q)) : xf;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) a3[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w3[b], xf, a3[b], 0, 0, 0);
+            xf = xn;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // epilogue: fp16(acc + b3) (+ rotary for q, k) into the staging rows, then one 16-B unit a thread
+        // (row, unit u: channels 8 u .. + 7, one head of one part) to its destination
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int c = 16 * (NB * wave + b) + 4 * q;
+            const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kB3 + c * 2);
+            f16x4 v = f16x4{lin_val(a3[b][0], b4[0]), lin_val(a3[b][1], b4[1]), lin_val(a3[b][2], b4[2]),
+                            lin_val(a3[b][3], b4[3])};
+            if constexpr (E3 == E3_QKV) {
+                if (c < 2 * NO) {  // q, k: rotary pairs (d, d + 1) from this row's tables
+                    const f16x4 cc = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + (r * kD + c % kD) * 2);
+                    const f16x4 ss = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + ((MT + r) * kD + c % kD) * 2);
+#pragma unroll
+                    for (int t = 0; t < 4; t += 2) rot_pair(v, t, cc[t], ss[t], cc[t + 1], ss[t + 1]);
+                }
+            }
+            *(__attribute__((address_space(3))) f16x4*)(lds + kS3 + r * (U3 * 16) + (((c >> 3) ^ r) << 4) + 8 * (q & 1)) = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int i = 0; i < (MT * U3 + 511) / 512; ++i) {
+            const int f = 512 * i + tid, row = f / U3, u = f % U3;
+            if (f < MT * U3 && m0 + row < p.m) {
+                const f16x8 v = *(lds_f16x8*)(lds + kS3 + row * (U3 * 16) + ((u ^ row) << 4));
+                const int c = 8 * u, grow = m0 + row;
+                f16* dst;
+                if constexpr (E3 == E3_PLAIN) {
+                    dst = c < q3.n_store ? q3.out[0] + (size_t)grow * q3.n_store + c : nullptr;
+                } else {
+                    const int part = c / NO, h = (c % NO) / kD;
+                    const LinRow lr = lin_row(p, grow, h);
+                    dst = q3.out[E3 == E3_QKV ? (lr.first ? 0 : 3) + part : (lr.first ? 0 : 1) + 2 * part] + lr.off + c % kD;
+                }
+                if (dst) *reinterpret_cast<f16x8*>(dst) = v;
+            }
+        }
+    }
+}
+
 // lg_ffn_pack: one thread per 16-B fragment of the packed stream (layout: include/lightglue_glue.h);
-// wave w's stream: 64 W1 pieces, 32 W2 pieces, then NB3 x 16 W3 pieces (NB3 = n3 / 256)
+// wave w's stream: 64 W1 pieces, 32 W2 pieces, then NB3 x 16 W3 pieces (NB3 = n3 / 256). form 0: the
+// 32-row kernel's fragments (32 channels x k16 a piece), form 1: the 16-row kernel's (16 x k32)
 __global__ __launch_bounds__(256) void ffn_pack_kernel(const f16* __restrict__ w1, const f16* __restrict__ w2,
-                                                       const f16* __restrict__ w3, int nb3, f16* packed) {
+                                                       const f16* __restrict__ w3, int nb3, int form, f16* packed) {
     const int np = 96 + 16 * nb3;                  // pieces per wave
     const int f = blockIdx.x * 256 + threadIdx.x;  // fragment: wave w, piece i, lane l
     if (f >= 8 * np * 64) return;
-    const int w = f / (np * 64), i = (f % (np * 64)) / 64, l = f % 64, r = l % 32, hh = l / 32;
+    const int w = f / (np * 64), i = (f % (np * 64)) / 64, l = f % 64;
     const f16* src;
-    if (i < 64) src = w1 + (size_t)(64 * w + 32 * (i & 1) + r) * 512 + 16 * (i >> 1) + 8 * hh;
-    else if (i < 96) src = w2 + (size_t)(32 * w + r) * 512 + 16 * (i - 64) + 8 * hh;
-    else {
-        const int j = (i - 96) / nb3, b = (i - 96) % nb3;
-        src = w3 + (size_t)(32 * (nb3 * w + b) + r) * 256 + 16 * j + 8 * hh;
+    if (form == 0) {
+        const int r = l % 32, hh = l / 32;
+        if (i < 64) src = w1 + (size_t)(64 * w + 32 * (i & 1) + r) * 512 + 16 * (i >> 1) + 8 * hh;
+        else if (i < 96) src = w2 + (size_t)(32 * w + r) * 512 + 16 * (i - 64) + 8 * hh;
+        else {
+            const int j = (i - 96) / nb3, b = (i - 96) % nb3;
+            src = w3 + (size_t)(32 * (nb3 * w + b) + r) * 256 + 16 * j + 8 * hh;
+        }
+    } else {
+        const int r = l % 16, q = l / 16;
+        if (i < 64) src = w1 + (size_t)(64 * w + 16 * (i & 3) + r) * 512 + 32 * (i >> 2) + 8 * q;
+        else if (i < 96) src = w2 + (size_t)(32 * w + 16 * ((i - 64) & 1) + r) * 512 + 32 * ((i - 64) >> 1) + 8 * q;
+        else {
+            const int j = (i - 96) / (2 * nb3), b = (i - 96) % (2 * nb3);
+            src = w3 + (size_t)(16 * (2 * nb3 * w + b) + r) * 256 + 32 * j + 8 * q;
+        }
     }
     *reinterpret_cast<f16x8*>(packed + (size_t)f * 8) = *reinterpret_cast<const f16x8*>(src);
 }
@@ -1617,12 +1887,19 @@ int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, what, hipGetErrorString(e));
 }
 
-// ffn_rows_kernel by size: 32-row workgroups up to one round of them (the most workgroups: latency),
-// 64-row beyond (half the weight bytes per row)
+// The one-launch FFN by size (lg_linear_set_ffn_fused 1): 16-row workgroups up to one round of them
+// (ffn_rows16_kernel: the most workgroups and the least vector work per CU, for latency), 32-row up
+// to one round, 64-row beyond (half the weight bytes per row); 2 / 3: the 32/64-row / 16-row kernel at
+// every size (A/B). wp: lg_ffn_pack's two layouts, the 32-row kernel's first.
 template <int E3, int NB3>
 void launch_ffn_rows(const LinArgs& p, const f16* gamma, const f16* beta, float eps, const f16* wp, const f16* b2,
                      const Proj3& q3, hipStream_t stream) {
-    if (p.m <= 32 * kTileGrid)
+    const int mode = g_ffn_fused.load();
+    if (mode == 3 || (mode != 2 && p.m <= 16 * kTileGrid)) {
+        const f16* wp16 = wp + (size_t)8 * (96 + 16 * NB3) * 1024 / 2;
+        hipLaunchKernelGGL((ffn_rows16_kernel<kFrDepth, E3, NB3>), dim3((p.m + 15) / 16), dim3(512), 0, stream, p, gamma, beta,
+                           eps, wp16, b2, q3);
+    } else if (p.m <= 32 * kTileGrid)
         hipLaunchKernelGGL((ffn_rows_kernel<1, kFrDepth, E3, NB3>), dim3((p.m + 31) / 32), dim3(512), 0, stream, p, gamma, beta,
                            eps, wp, b2, q3);
     else
@@ -1729,8 +2006,8 @@ int32_t lg_linear_cat_ffn(const void* x, const void* ctx0, const void* ctx1, int
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_linear_cat_ffn", hipGetErrorString(e));
 }
 
-size_t lg_ffn_packed_bytes(int32_t heads, int32_t n3) {
-    return heads == 4 && (n3 == 0 || n3 == 512 || n3 == 768) ? (size_t)8 * (96 + n3 / 16) * 1024 : 0;
+size_t lg_ffn_packed_bytes(int32_t heads, int32_t n3) {  // both layouts, the 32-row kernel's first
+    return heads == 4 && (n3 == 0 || n3 == 512 || n3 == 768) ? (size_t)2 * 8 * (96 + n3 / 16) * 1024 : 0;
 }
 
 int32_t lg_ffn_pack(const void* w1, const void* w2, const void* w3, int32_t n3, int32_t heads, void* packed, hipStream_t stream) {
@@ -1738,8 +2015,9 @@ int32_t lg_ffn_pack(const void* w1, const void* w2, const void* w3, int32_t n3, 
         (n3 && (!w3 || !aligned16(w3))))
         return bad("lg_ffn_pack");
     const int nb3 = n3 / 256, frags = 8 * (96 + 16 * nb3) * 64;
-    hipLaunchKernelGGL(ffn_pack_kernel, dim3((frags + 255) / 256), dim3(256), 0, stream, (const f16*)w1, (const f16*)w2,
-                       (const f16*)w3, nb3, (f16*)packed);
+    for (int form = 0; form < 2; ++form)
+        hipLaunchKernelGGL(ffn_pack_kernel, dim3((frags + 255) / 256), dim3(256), 0, stream, (const f16*)w1, (const f16*)w2,
+                           (const f16*)w3, nb3, form, (f16*)packed + (size_t)form * frags * 8);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_ffn_pack", hipGetErrorString(e));
@@ -1881,6 +2159,6 @@ int32_t lg_diag_fr_stamps(void* host_dst) {  // (diagnostic build only: not in t
 }
 #endif
 int32_t lg_linear_set_ln_fused(int32_t on) { return g_ln_fused.exchange(on == 2 ? 2 : on ? 1 : 0); }
-int32_t lg_linear_set_ffn_fused(int32_t on) { return g_ffn_fused.exchange(on ? 1 : 0); }
+int32_t lg_linear_set_ffn_fused(int32_t mode) { return g_ffn_fused.exchange(mode >= 0 && mode <= 3 ? mode : 1); }
 
 }  // extern "C"

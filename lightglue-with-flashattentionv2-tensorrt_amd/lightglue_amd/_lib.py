@@ -171,7 +171,7 @@ class LibraryMissing(RuntimeError):
     pass
 
 
-GLUE_ABI_VERSION = 3  # include/lightglue_glue.h LG_GLUE_ABI_VERSION
+GLUE_ABI_VERSION = 4  # include/lightglue_glue.h LG_GLUE_ABI_VERSION
 
 
 def load() -> ctypes.CDLL:

@@ -311,17 +311,24 @@ def _ffn_in_fused(block: nn.Module, proj: nn.Linear, dtype: torch.dtype):
 
 
 def ffn_pack(w1: torch.Tensor, w2: torch.Tensor, w3: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """The one-launch FFN's weight stream (lg_ffn_pack, include/lightglue_glue.h) by tensor ops: for
-    wave w of 8, W1 rows 64w.. as pieces (step j, block b), then W2 rows 32w.. as pieces (step j), then
-    (lg_linear_cat_ffn_proj) W3 rows (n3/8)w.. as pieces (step j, block b); each piece's 16-B lane l =
-    W[row0 + 32b + l % 32][16j + 8(l // 32) : + 8]."""
-    p1 = w1.reshape(8, 2, 32, 32, 2, 8).permute(0, 3, 1, 4, 2, 5)   # (w, j, b, hh, r, e)
-    p2 = w2.reshape(8, 32, 32, 2, 8).permute(0, 2, 3, 1, 4)         # (w, j, hh, r, e)
-    parts = [p1.reshape(8, -1), p2.reshape(8, -1)]
+    """The one-launch FFN's weight streams (lg_ffn_pack, include/lightglue_glue.h) by tensor ops, the
+    32-row kernel's layout then the 16-row kernel's. 32-row: for wave w of 8, W1 rows 64w.. as pieces
+    (step j, block b), then W2 rows 32w.. as pieces (step j), then (lg_linear_cat_ffn_proj) W3 rows
+    (n3/8)w.. as pieces (step j, block b); each piece's 16-B lane l = W[row0 + 32b + l % 32][16j +
+    8(l // 32) : + 8]. 16-row: the same rows per wave in 16-row blocks and k32 steps, lane l =
+    W[row0 + 16b + l % 16][32j + 8(l // 16) : + 8]."""
+    def layout(rows, k):  # W [8 waves * blocks * rows, steps * k] -> (w, step, block, lane group, row, e)
+        def f(w):
+            nb = w.shape[0] // (8 * rows)
+            g = k // 8
+            return w.reshape(8, nb, rows, w.shape[1] // k, g, 8).permute(0, 3, 1, 4, 2, 5).reshape(8, -1)
+        return f
+    parts32 = [layout(32, 16)(w1), layout(32, 16)(w2)]
+    parts16 = [layout(16, 32)(w1), layout(16, 32)(w2)]
     if w3 is not None:
-        nb3 = w3.shape[0] // 256
-        parts.append(w3.reshape(8, nb3, 32, 16, 2, 8).permute(0, 3, 1, 4, 2, 5).reshape(8, -1))  # (w, j, b, hh, r, e)
-    return torch.cat(parts, 1).reshape(-1).contiguous()
+        parts32.append(layout(32, 16)(w3))
+        parts16.append(layout(16, 32)(w3))
+    return torch.cat([torch.cat(parts32, 1).reshape(-1), torch.cat(parts16, 1).reshape(-1)]).contiguous()
 
 
 def _ffn_packed(block: nn.Module, proj: nn.Linear, dtype: torch.dtype, w3=None):

@@ -491,10 +491,13 @@ def test_ffn_and_form_hooks_validate_before_touching_the_device(lib):
         assert lib.lg_linear_set_wide(4) == -1
     finally:
         lib.lg_linear_set_wide(prev)
-    prev = lib.lg_linear_set_ffn_fused(7)         # any nonzero: 1
+    prev = lib.lg_linear_set_ffn_fused(7)         # outside 0..3: 1
     try:
         assert lib.lg_linear_set_ffn_fused(0) == 1
-        assert lib.lg_linear_set_ffn_fused(1) == 0
+        assert lib.lg_linear_set_ffn_fused(3) == 0
+        assert lib.lg_linear_set_ffn_fused(2) == 3
+        assert lib.lg_linear_set_ffn_fused(-1) == 2
+        assert lib.lg_linear_set_ffn_fused(1) == 1
     finally:
         lib.lg_linear_set_ffn_fused(prev)
 

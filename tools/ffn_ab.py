@@ -1,5 +1,5 @@
 """A/B timing of lg_linear_cat_ffn's forms (lg_linear_set_ffn_fused: 0 its two calls, 1 the one-launch
-ffn_rows_kernel) — the op alone at P pairs of
+form by size, 2 ffn_rows_kernel (32 / 64 rows), 3 ffn_rows16_kernel) — the op alone at P pairs of
 n keypoints (a graph of back-to-back calls per form, replays interleaved), then whole fp16 matcher
 forwards (graph replay, interleaved), with the max |difference| of each form's outputs from the first.
 
