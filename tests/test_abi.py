@@ -463,8 +463,10 @@ def test_ffn_and_form_hooks_validate_before_touching_the_device(lib):
     for bad in (dict(x=None), dict(w2=None), dict(h=None), dict(out=A), dict(out=A + 4), dict(heads=0),
                 dict(heads=3), dict(pairs=-1), dict(eps=-1.0), dict(x=A + 8), dict(wp=A + 8)):
         assert call(**{**bad, "pairs": 0 if "pairs" not in bad else bad["pairs"]}) == 1, bad
-    assert lib.lg_ffn_packed_bytes(4, 0) == (512 * 512 + 256 * 512) * 2 and lib.lg_ffn_packed_bytes(3, 0) == 0
-    assert lib.lg_ffn_packed_bytes(4, 768) == (512 * 512 + 256 * 512 + 768 * 256) * 2 and lib.lg_ffn_packed_bytes(4, 384) == 0
+    # (two layouts: the 32-row kernel's, then the 16-row kernel's)
+    assert lib.lg_ffn_packed_bytes(4, 0) == 2 * (512 * 512 + 256 * 512) * 2 and lib.lg_ffn_packed_bytes(3, 0) == 0
+    assert lib.lg_ffn_packed_bytes(4, 768) == 2 * (512 * 512 + 256 * 512 + 768 * 256) * 2
+    assert lib.lg_ffn_packed_bytes(4, 384) == 0
     for bad in ((A, A, None, 0, 3, A), (None, A, None, 0, 4, A), (A, A, None, 0, 4, None), (A, A + 4, None, 0, 4, A),
                 (A, A, None, 512, 4, A), (A, A, A + 8, 768, 4, A), (A, A, A, 256, 4, A)):
         assert lib.lg_ffn_pack(*bad, None) == 1, bad

@@ -122,30 +122,50 @@ def test_pair_inputs_fast_path_needs_every_operand_fp16():
 
 
 def test_ffn_pack_layout():
-    """ffn_pack (the one-launch FFN's weight stream, include/lightglue_glue.h lg_ffn_pack): wave w's
-    96 KiB = W1 pieces i = 2j + b, then W2 pieces 64 + j; lane l of a piece = W[row0 + 32b + l % 32]
-    [16j + 8(l // 32) : + 8]. Every fragment checked against that definition."""
+    """ffn_pack (the one-launch FFN's weight streams, include/lightglue_glue.h lg_ffn_pack), two layouts
+    back to back. 32-row kernel: wave w's 96 KiB = W1 pieces i = 2j + b, then W2 pieces 64 + j, then
+    W3 pieces 96 + nb3 j + b; lane l of a piece = W[row0 + 32b + l % 32][16j + 8(l // 32) : + 8].
+    16-row kernel: W1 pieces 4j + b, W2 64 + 2j + b, W3 96 + 2 nb3 j + b; lane l = W[row0 + 16b + l % 16]
+    [32j + 8(l // 16) : + 8]. Every fragment checked against those definitions."""
     from lightglue_amd import matcher
 
     w1 = torch.arange(512 * 512, dtype=torch.float32).reshape(512, 512)
     w2 = -torch.arange(256 * 512, dtype=torch.float32).reshape(256, 512)
-    got = matcher.ffn_pack(w1, w2).reshape(8, 96, 64, 8)
-    w, i, l = torch.meshgrid(torch.arange(8), torch.arange(96), torch.arange(64), indexing="ij")
-    r, hh = l % 32, l // 32
     e = torch.arange(8)
-    j1, b = (i // 2).clamp(max=31), i % 2
-    exp1 = w1[(64 * w + 32 * b + r)[..., None], (16 * j1 + 8 * hh)[..., None] + e]
-    exp2 = w2[(32 * w + r)[..., None].clamp(max=255), (16 * (i - 64).clamp(min=0) + 8 * hh)[..., None] + e]
-    assert torch.equal(got, torch.where((i < 64)[..., None], exp1, exp2))
-    for n3 in (512, 768):  # lg_linear_cat_ffn_proj's W3 after W2: piece 96 + nb3 j + b
-        w3 = torch.arange(n3 * 256, dtype=torch.float32).reshape(n3, 256) + 0.5
-        nb3 = n3 // 256
-        got = matcher.ffn_pack(w1, w2, w3).reshape(8, 96 + 16 * nb3, 64, 8)
-        assert torch.equal(got[:, :96], matcher.ffn_pack(w1, w2).reshape(8, 96, 64, 8))
-        w, i, l = torch.meshgrid(torch.arange(8), torch.arange(16 * nb3), torch.arange(64), indexing="ij")
-        j, b, r, hh = i // nb3, i % nb3, l % 32, l // 32
-        exp3 = w3[(32 * (nb3 * w + b) + r)[..., None], (16 * j + 8 * hh)[..., None] + e]
-        assert torch.equal(got[:, 96:], exp3)
+
+    def expected(w3, form):
+        nb3 = 0 if w3 is None else w3.shape[0] // 256
+        np_ = 96 + 16 * nb3
+        w, i, l = torch.meshgrid(torch.arange(8), torch.arange(np_), torch.arange(64), indexing="ij")
+        if form == 32:
+            r, g = l % 32, l // 32
+            j1, b1 = i // 2, i % 2
+            j2, b2 = i - 64, 0 * i
+            j3, b3 = (i - 96) // max(nb3, 1), (i - 96) % max(nb3, 1)
+            row1, k1 = 64 * w + 32 * b1 + r, 16 * j1 + 8 * g
+            row2, k2 = 32 * w + r, 16 * j2 + 8 * g
+            row3, k3 = 32 * (nb3 * w + b3) + r, 16 * j3 + 8 * g
+        else:
+            r, g = l % 16, l // 16
+            j1, b1 = i // 4, i % 4
+            j2, b2 = (i - 64) // 2, (i - 64) % 2
+            j3, b3 = (i - 96) // max(2 * nb3, 1), (i - 96) % max(2 * nb3, 1)
+            row1, k1 = 64 * w + 16 * b1 + r, 32 * j1 + 8 * g
+            row2, k2 = 32 * w + 16 * b2 + r, 32 * j2 + 8 * g
+            row3, k3 = 16 * (2 * nb3 * w + b3) + r, 32 * j3 + 8 * g
+        out = torch.zeros(8, np_, 64, 8)
+        m1, m2, m3 = i < 64, (i >= 64) & (i < 96), i >= 96
+        out[m1] = w1[row1[m1][:, None], k1[m1][:, None] + e]
+        out[m2] = w2[row2[m2][:, None], k2[m2][:, None] + e]
+        if nb3:
+            out[m3] = w3[row3[m3][:, None], k3[m3][:, None] + e]
+        return out
+
+    for n3 in (0, 512, 768):
+        w3 = None if n3 == 0 else torch.arange(n3 * 256, dtype=torch.float32).reshape(n3, 256) + 0.5
+        got = matcher.ffn_pack(w1, w2, w3).reshape(2, 8, 96 + n3 // 16, 64, 8)
+        assert torch.equal(got[0], expected(w3, 32)), n3
+        assert torch.equal(got[1], expected(w3, 16)), n3
 
 
 def _gpu_run(name, dtype, glue="hip"):
