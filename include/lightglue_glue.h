@@ -170,13 +170,14 @@ int32_t lg_log_double_softmax_f16(const void* sim, const void* z0, const void* z
                                   int64_t z_row_stride, int32_t m, int32_t n, int32_t batch, float* scores,
                                   void* workspace, hipStream_t stream);
 
-/* The fp16 assignment head in three launches (round 6): v [batch][m + n][ld] fp16 is the final
+/* The fp16 assignment head in two launches (round 6): v [batch][m + n][ld] fp16 is the final
  * projection of both images' rows (image 0's m rows, then image 1's n; pairs pair_stride elements
  * apart), channels 0..255 the scaled descriptors m0 / m1 (final_proj(d) / d^0.25) and channel zc
  * (>= 256) the matchability logit. scores [batch, m, n] fp32 = log_softmax(sim, 2) + log_softmax(sim, 1)
  * + logsig(z0) + logsig(z1)ᵀ with sim = m0 · m1ᵀ rounded to fp16 (lightglue.py:208-233): the similarity
  * by MFMA with each row's and column's (max, sum of exponentials) over shares of the other image (a
- * workgroup owns 32 rows of one image), the logsumexps closed once per row and column, the combine.
+ * workgroup owns 32 rows of one image), then the combine, which closes its rows' and columns'
+ * logsumexps from those partials.
  * m, n <= 2048, n % 8 == 0, ld % 8 == 0; v, scores, workspace 16-B aligned; workspace >=
  * lg_assign_scores_workspace(m, n, batch) bytes (its first batch * m * n * 2 bytes: sim, fp16). */
 size_t lg_assign_scores_workspace(int32_t m, int32_t n, int32_t batch);

@@ -1302,6 +1302,11 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 15, q = lane >> 4;
     const int m0 = blockIdx.x * MT;
+#ifdef LG_FR_STAMPS
+    unsigned long long fr_[6] = {0, 0, 0, 0, 0, 0}, fr_last_, fr_entry_;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fr_entry_)::"memory");
+    fr_last_ = fr_entry_;
+#endif
     auto tile_unit = [](int row, int u) { return row * 1024 + ((u ^ (row & 15)) << 4); };  // A / h tiles
     auto x_unit = [](int row, int u) { return row * 512 + ((u ^ (row & 15)) << 4); };      // x' tile
 
@@ -1363,6 +1368,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
     if (tid < NV3) *(lds_f16x8*)(lds + kB3 + tid * 16) = v3;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    FR_SEG(0);
 
     // ---- phase 1: hᵀ (the wave's 64 channels x 16 rows) = W1 · Aᵀ, k32 steps, B read a step ahead ----
     f32x4 acc[4] = {};
@@ -1378,6 +1384,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         bf = bn;
         __builtin_amdgcn_sched_barrier(0);
     }
+    FR_SEG(1);
 
     // ---- LayerNorm: lane (r, q) holds channels 64 w + 16 b + 4 q + t of row r; h = fp16(acc + b1) in
     // one rounding, the row's sum and sum of squares over the 4 q lanes, then the 8 waves via LDS ----
@@ -1431,6 +1438,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // h complete
+    FR_SEG(2);
 
     // ---- phase 2: outᵀ (the wave's 32 channels x 16 rows) = W2 · hᵀ ----
     f32x4 o2[2] = {};
@@ -1444,6 +1452,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         hf = hn;
         __builtin_amdgcn_sched_barrier(0);
     }
+    FR_SEG(3);
     // ---- out = fp16(fp16(acc + b2) + x): fp16(acc + b2) into the x' tile, then one 16-B unit a thread
     // (row tid / 32, unit tid % 32) with x from the A tile, to memory and back into the x' tile ----
 #pragma unroll
@@ -1465,6 +1474,10 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         if (m0 + row < p.m) *reinterpret_cast<f16x8*>(p.out[0] + (size_t)(m0 + row) * NO + 8 * u) = v;
         if constexpr (E3 != E3_NONE) *(lds_f16x8*)(lds + kX + x_unit(row, u)) = v;
     }
+#ifdef LG_FR_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FR_SEG(4);
+#endif
     if constexpr (E3 != E3_NONE) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // x' complete
@@ -1520,6 +1533,17 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
             }
         }
     }
+#ifdef LG_FR_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FR_SEG(5);
+    if (lane == 0 && blockIdx.x < 256) {
+        unsigned long long* d = g_fr_stamps + ((size_t)blockIdx.x * 8 + wave) * 8;
+        for (int i = 0; i < 5; ++i) d[i] = fr_[i];
+        d[5] = fr_last_ - fr_entry_;
+        d[6] = fr_entry_;
+        d[7] = fr_[5];
+    }
+#endif
 }
 
 // lg_ffn_pack: one thread per 16-B fragment of the packed stream (layout: include/lightglue_glue.h);
@@ -1565,8 +1589,8 @@ __global__ __launch_bounds__(256) void ffn_pack_kernel(const f16* __restrict__ w
 //    column partials: no cross-workgroup exchange. (An image-1 workgroup recomputes its columns of sim
 //    with the operands swapped: the same products in the same k-step order.) S splits of the other
 //    image fill the chip at a single pair (each workgroup then streams 1/S of it).
-//  * assign_close_kernel closes the S partials of each row and column (fixed order) into the terms
-//    logsig(z) - logsumexp, once; assign_combine_kernel writes scores = 2 sim + row term + column term.
+//  * assign_combine_kernel closes the S partials of its rows and columns (fixed order) into the terms
+//    logsig(z) - logsumexp and writes scores = 2 sim + row term + column term.
 struct AsArgs {
     const f16* v;     // [batch][m + n][ld]: image 0's rows then image 1's; channels 0..255 the scaled
                       // final projection, channel zc the matchability logit
@@ -1575,8 +1599,8 @@ struct AsArgs {
     f16* sim;         // workspace [batch][m][n]
     float2* rpart;    // workspace [batch][S][m]: (max, sum of exp) of row i over split s
     float2* cpart;    // workspace [batch][S][n]: the same for column j
-    float* rterm;     // workspace [batch][m]: logsig(z0[i]) - lse_row[i]
-    float* cterm;     // workspace [batch][n]: logsig(z1[j]) - lse_col[j]
+    float* rterm;     // workspace [batch][m] (round 6's separate close; kept in the workspace layout)
+    float* cterm;     // workspace [batch][n]
     float* scores;    // [batch][m][n]
 };
 __device__ __forceinline__ float log_sigmoid_f(float z) { return fminf(z, 0.f) - log1pf(__expf(-fabsf(z))); }
@@ -1701,61 +1725,69 @@ __global__ __launch_bounds__(512, 1) void assign_lse_kernel(AsArgs a) {
     }
 }
 
-// the logsumexp of S (max, sum) partials, merged in split order
+// the logsumexp of S (max, sum) partials, merged in split order; every partial's load issued before
+// the merge (round 6's first combine-side close walked them one dependent load at a time: 18-38 us)
 __device__ __forceinline__ float lse_close(const float2* part, size_t stride, int S) {
+    float2 q[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q[k] = k < S ? part[k * stride] : make_float2(-INFINITY, 0.f);
     float mx = -INFINITY, s = 0.f;
-    for (int k = 0; k < S; ++k) {
-        const float2 q = part[k * stride];
-        if (q.x == -INFINITY) continue;
-        if (q.x > mx) {
-            s = s * __expf(mx - q.x) + q.y;
-            mx = q.x;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        if (q[k].x == -INFINITY) continue;
+        if (q[k].x > mx) {
+            s = s * __expf(mx - q[k].x) + q[k].y;
+            mx = q[k].x;
         } else {
-            s += q.y * __expf(q.x - mx);
+            s += q[k].y * __expf(q[k].x - mx);
         }
     }
     return mx + __logf(s);
 }
 
-// the row and column terms once: term = logsig(z) - logsumexp closed from the S partials (one thread
-// per row of image 0, then per column)
-__global__ __launch_bounds__(256) void assign_close_kernel(AsArgs a) {
-    const int p = blockIdx.y, t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= a.m + a.n) return;
-    const f16* const vp = a.v + (size_t)p * a.ps;
-    const float z = (float)vp[(size_t)t * a.ld + a.zc];  // (row t of v: image 0's rows, then image 1's)
-    if (t < a.m) a.rterm[(size_t)p * a.m + t] = log_sigmoid_f(z) - lse_close(a.rpart + (size_t)p * a.S * a.m + t, a.m, a.S);
-    else a.cterm[(size_t)p * a.n + t - a.m] = log_sigmoid_f(z) - lse_close(a.cpart + (size_t)p * a.S * a.n + t - a.m, a.n, a.S);
-}
-
-// scores = 2 sim + rterm[i] + cterm[j] (fp32). A block is 8 W rows x 512 columns; each wave writes 8
-// rows, a lane 8 columns (16-B loads, 2 x 16-B stores)
+// scores = 2 sim + rterm[i] + cterm[j] (fp32), the terms logsig(z) - logsumexp closed here from the S
+// partials (round 6: a separate close launch cost ~4.7 us at a single pair): the block's 8 W rows'
+// and 512 columns' terms into LDS (256 threads; every partial and z load in flight at once), then each
+// of the W combine waves writes 8 rows, a lane 8 columns (16-B loads, 2 x 16-B stores)
 template <int W>
-__global__ __launch_bounds__(64 * W) void assign_combine_kernel(AsArgs a) {
-    const int p = blockIdx.z;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int i0 = (blockIdx.x * W + wave) * 8, j = blockIdx.y * 512 + lane * 8;
-    if (i0 >= a.m || j >= a.n) return;
+__global__ __launch_bounds__(256) void assign_combine_kernel(AsArgs a) {
+    __shared__ float rts[8 * W], cts[512];
+    const int p = blockIdx.z, tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int ib = blockIdx.x * 8 * W, jb = blockIdx.y * 512;
+    const f16* const vp = a.v + (size_t)p * a.ps;
+    if (tid < 8 * W && ib + tid < a.m) {
+        const float z = (float)vp[(size_t)(ib + tid) * a.ld + a.zc];
+        rts[tid] = log_sigmoid_f(z) - lse_close(a.rpart + (size_t)p * a.S * a.m + ib + tid, a.m, a.S);
+    }
+#pragma unroll
+    for (int c = tid; c < 512; c += 256) {
+        if (jb + c < a.n) {
+            const float z = (float)vp[(size_t)(a.m + jb + c) * a.ld + a.zc];
+            cts[c] = log_sigmoid_f(z) - lse_close(a.cpart + (size_t)p * a.S * a.n + jb + c, a.n, a.S);
+        }
+    }
+    __syncthreads();
+    const int i0 = ib + wave * 8, j = jb + lane * 8;
+    if (wave >= W || i0 >= a.m || j >= a.n) return;
     const int i1 = min(i0 + 8, a.m);
     const f16* sim = a.sim + (size_t)p * a.m * a.n;
     float* out = a.scores + (size_t)p * a.m * a.n;
     f16x8 x[8];
-    float rt[8];
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-        const int i = min(i0 + b, i1 - 1);
-        x[b] = *reinterpret_cast<const f16x8*>(sim + (size_t)i * a.n + j);
-        rt[b] = a.rterm[(size_t)p * a.m + i];
-    }
-    const f32x4 cl = *(const f32x4*)(a.cterm + (size_t)p * a.n + j), ch = *(const f32x4*)(a.cterm + (size_t)p * a.n + j + 4);
+    for (int b = 0; b < 8; ++b) x[b] = *reinterpret_cast<const f16x8*>(sim + (size_t)min(i0 + b, i1 - 1) * a.n + j);
+    float cl[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cl[e] = cts[lane * 8 + e];
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
         if (i0 + b >= i1) break;
+        const float rt = rts[wave * 8 + b];
         f32x4 o0, o1;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            o0[e] = 2.f * (float)x[b][e] + rt[b] + cl[e];
-            o1[e] = 2.f * (float)x[b][e + 4] + rt[b] + ch[e];
+            o0[e] = 2.f * (float)x[b][e] + rt + cl[e];
+            o1[e] = 2.f * (float)x[b][e + 4] + rt + cl[e + 4];
         }
         *reinterpret_cast<f32x4*>(out + (size_t)(i0 + b) * a.n + j) = o0;
         *reinterpret_cast<f32x4*>(out + (size_t)(i0 + b) * a.n + j + 4) = o1;
@@ -2097,13 +2129,13 @@ int32_t lg_assign_scores(const void* v, int64_t pair_stride, int32_t ld, int32_t
     else if (bpw <= 2) hipLaunchKernelGGL(assign_lse_kernel<2>, g1, dim3(512), 0, stream, a);
     else if (bpw <= 4) hipLaunchKernelGGL(assign_lse_kernel<4>, g1, dim3(512), 0, stream, a);
     else hipLaunchKernelGGL(assign_lse_kernel<8>, g1, dim3(512), 0, stream, a);
-    hipLaunchKernelGGL(assign_close_kernel, dim3((m + n + 255) / 256, batch), dim3(256), 0, stream, a);
-    // combine: blocks of 8 W rows x 512 columns (W = 4: 32 rows; 1 where that leaves the chip idle)
+    // combine (with the row / column closes): blocks of 8 W rows x 512 columns (W = 4: 32 rows; 1 where
+    // that leaves the chip idle)
     const int cb = (n + 511) / 512;
     if ((long)((m + 31) / 32) * cb * batch >= 128)
         hipLaunchKernelGGL(assign_combine_kernel<4>, dim3((m + 31) / 32, cb, batch), dim3(256), 0, stream, a);
     else
-        hipLaunchKernelGGL(assign_combine_kernel<1>, dim3((m + 7) / 8, cb, batch), dim3(64), 0, stream, a);
+        hipLaunchKernelGGL(assign_combine_kernel<1>, dim3((m + 7) / 8, cb, batch), dim3(256), 0, stream, a);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MHA_HD64_STATUS_SUCCESS
                            : mha_hd64::report_error(MHA_HD64_STATUS_LAUNCH_FAILED, "lg_assign_scores", hipGetErrorString(e));

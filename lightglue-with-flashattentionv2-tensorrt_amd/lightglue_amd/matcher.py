@@ -662,15 +662,18 @@ class LightGlueMatcher(nn.Module):
     # to_qk | to_v, q: the next layer's Wqkv, h: the head's projection). Measured
     # (profiles/r06/chain_kinds_forward_ab.jsonl, ms per forward, none / s / h / sh / sqh): P = 1 n = 1024
     # 0.496 / 0.481 / 0.494 / 0.480 / 0.492, P = 4 0.790 / 0.729 / 0.747 / 0.723 / 0.772, P = 16 2.165 /
-    # 2.133 / 2.163 / 2.128 / 2.183: "sh" everywhere; folding Wqkv (768 channels, 384 KiB more per
-    # workgroup's stream) costs the launch more than the separate projection takes. Outputs bitwise
-    # equal in every form. LG_CHAIN (or this attribute) overrides, for A/B.
+    # 2.133 / 2.163 / 2.128 / 2.183: "sh" with the 32-row FFN kernel; folding Wqkv (768 channels, 384 KiB
+    # more per workgroup's stream) cost the launch more than the separate projection took. With the
+    # 16-row kernel (2,048..4,096 rows: twice the workgroups) "sqh" wins (profiles/r06/chain_kinds_rows16_ab
+    # .jsonl, sh / sqh: P = 1 n = 1024 0.445 / 0.439, n = 2048 0.707 / 0.673, P = 2 0.588 / 0.558; n = 512
+    # 0.375 / 0.383, P = 4 0.767 / 0.765). Outputs bitwise equal in every form. LG_CHAIN (or this
+    # attribute) overrides, for A/B.
     chain_kinds: Optional[str] = None
 
     def _chain_kinds(self, rows: int) -> str:
         if self.chain_kinds is not None:
             return self.chain_kinds
-        return os.environ.get("LG_CHAIN", "sh")
+        return os.environ.get("LG_CHAIN", "sqh" if 2048 <= rows <= 4096 else "sh")
 
     def chain_ok(self, x: torch.Tensor, m: int, n: int) -> bool:
         """The chained fp16 path: every block fusable (4 x 64 heads, d = 256) and the fp16 head."""

@@ -7,17 +7,26 @@ seams inside the graph), summed by kernel family.
 Without a count, one forward is cut at the assignment head's combine pass (its last kernel, once per forward)."""
 import csv
 import sys
+import re
 from collections import defaultdict
+
+
+E3_NAMES = {"0": "", "1": " +split2", "2": " +qkv", "3": " +head"}
 
 
 def family(name):
     n = name.removeprefix("void ").replace("(anonymous namespace)::", "").replace("mha_hd64::", "")
     for k in ("mha_hd64_stream_kernel", "mha_hd64_direct16_kernel", "mha_hd64_direct_kernel", "mha_hd64_fwd_kernel",
-              "linear_tile_kernel", "linear_kernel", "linear_ln_kernel", "ffn_rows_kernel", "assign_lse_kernel",
-              "assign_combine_kernel", "ln_gelu", "lse16", "combine16", "pair_inputs", "Cijk"):
+              "linear_tile_kernel", "linear_kernel", "linear_ln_kernel", "ffn_rows16_kernel", "ffn_rows_kernel",
+              "assign_lse_kernel", "assign_close_kernel", "assign_combine_kernel", "ln_gelu", "lse16", "combine16",
+              "pair_inputs", "Cijk"):
         if k in n:
             if k.startswith("linear") and k != "linear_ln_kernel":
                 return n.split("(")[0]
+            if k.startswith("ffn_rows"):  # the phase-3 kind: the E3 template argument (demangled or not)
+                m = re.search(r"ffn_rows(?:16)?_kernel<(?:\d+, )?\d+, (\d+), \d+>", n) or \
+                    re.search(r"ffn_rows(?:16)?_kernelI(?:Li\d+E)?Li\d+ELi(\d+)ELi\d+E", n)
+                return k + (E3_NAMES.get(m.group(1), "") if m else "")
             return k
     return "FW " + n.split("(")[0][:60]
 

@@ -4,7 +4,8 @@ cycles of chained segments; see csrc/lightglue_linear.hip).
     MHA_HD64_LIB=lib/ab/libmha_hd64_frstamps.so python tools/fr_stamps.py [P=1] [n=1024] [kind=0]
 
 kind 0: lg_linear_cat_ffn; 1 / 2 / 3: lg_linear_cat_ffn_proj with the split2 / qkv / plain projection
-(segment "phase3": the projection and its epilogue).
+(segment "phase3": the projection and its epilogue). The kernel is the one lg_linear_cat_ffn picks
+by size (ffn_rows16_kernel up to 4,096 rows).
 """
 import ctypes
 import json
@@ -47,7 +48,10 @@ def main():
         return mt._Hip.ffn_proj(x, c0, c1, b, ln, b2, wp, kind, b3, (n, n, P), cs, sn, 384)
 
     names = ["prologue", "phase1", "layernorm_gelu", "phase2", "epilogue", "total", "entry", "phase3"]
-    wgs = min(256, (M + 31) // 32 if M <= 8192 else (M + 63) // 64)  # (stamps of the first 256)
+    mode = lib.lg_linear_set_ffn_fused(1)  # (the form in force; restored at once)
+    lib.lg_linear_set_ffn_fused(mode)
+    rows16 = mode == 3 or (mode != 2 and M <= 4096)
+    wgs = min(256, (M + 15) // 16 if rows16 else (M + 31) // 32 if M <= 8192 else (M + 63) // 64)  # (the first 256)
     rows = []
     for rep in range(6):
         for _ in range(3):  # back to back, as in a forward
@@ -59,7 +63,7 @@ def main():
         if rep:
             rows.append(a)
     a = np.concatenate(rows, 0)
-    out = {"P": P, "n": n, "M": M, "kind": kind, "workgroups": wgs,
+    out = {"P": P, "n": n, "M": M, "kind": kind, "kernel": "ffn_rows16" if rows16 else "ffn_rows", "workgroups": wgs,
            "median_cycles": {k: float(np.median(a[:, :, i])) for i, k in enumerate(names) if k != "entry"},
            "max_total": float(a[:, :, 5].max()),
            "entry_spread_cycles": float(np.median(a[:, :, 6].max(1) - a[:, :, 6].min(1)))}
