@@ -1922,7 +1922,10 @@ int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
 // The one-launch FFN by size (lg_linear_set_ffn_fused 1): 16-row workgroups up to one round of them
 // (ffn_rows16_kernel: the most workgroups and the least vector work per CU, for latency), 32-row up
 // to one round, 64-row beyond (half the weight bytes per row); 2 / 3: the 32/64-row / 16-row kernel at
-// every size (A/B). wp: lg_ffn_pack's two layouts, the 32-row kernel's first.
+// every size (A/B). wp: lg_ffn_pack's two layouts, the 32-row kernel's first. (Tried and dropped: the
+// 32-row kernel two workgroups per CU (128 VGPRs, an 8-piece ring, staging over h), for one workgroup's
+// A-tile latency under the other's stream — 46.0 -> 47.1 us at 32,768 rows, 23.0 -> 24.1 at 16,384,
+// equal bits; profiles/r06/ffn_rows_occ2_ab.jsonl.)
 template <int E3, int NB3>
 void launch_ffn_rows(const LinArgs& p, const f16* gamma, const f16* beta, float eps, const f16* wp, const f16* b2,
                      const Proj3& q3, hipStream_t stream) {

@@ -4,6 +4,10 @@
 #   bash tools/gpu/session.sh <tag> <step> [<step> ...]
 # steps: tests[:<pytest -k expr>]  gpu  ffn_ab[:<args>]  bench[:<args>]  smoke  prof_fwd:<P>x<n>
 #        pmc_ffn:<P>:<n>:<mode>  "tool:<tools/NAME.py> [args...]" (one quoted word)
+#        "frstamps:<P> <n> <kind>" (FFN segment stamps; build lib/ab/libmha_hd64_frstamps.so first with
+#        tools/build_linear_variant.sh frstamps -DLG_FR_STAMPS)
+# (the round-start check: gpu smoke "bench:--steps 20 --warmup 5"; round 5's 50 tools/gpu/r05_*.sh
+# sessions were each one such list of steps, folded into this script in round 6)
 set -o pipefail
 tag=$1; shift
 O=$PWD/gpurun_out/$tag; mkdir -p "$O"
@@ -27,6 +31,10 @@ for step in "$@"; do
         tool)   # one diagnostic script of tools/ (its stdout in <name>.log)
             read -r -a ta <<< "$arg"; tn=${ta[0]}; sfx=$(basename -a "${ta[@]:1}" 2>/dev/null | tr -c 'a-zA-Z0-9\n' '_' | tr '\n' '_')
             run 600 "${tn}_${sfx:0:60}.log" python -u "tools/${tn}.py" "${ta[@]:1}" || exit $? ;;
+        frstamps)
+            run 120 "frstamps_${arg// /_}.log" env MHA_HD64_LIB=$PWD/lightglue-with-flashattentionv2-tensorrt_amd/lib/ab/libmha_hd64_frstamps.so \
+                python -u tools/fr_stamps.py $arg || exit $?
+            grep '^{' "$O/frstamps_${arg// /_}.log" >> "$O/stamps.jsonl" ;;
         smoke)  run 300 smoke.log python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
         prof_fwd)  # kernel trace of P x n forwards (graph replays), then one forward's timeline
             P=${arg%x*}; n=${arg#*x}; R=$PWD
