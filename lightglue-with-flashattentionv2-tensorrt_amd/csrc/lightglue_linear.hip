@@ -1303,7 +1303,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
     const int r = lane & 15, q = lane >> 4;
     const int m0 = blockIdx.x * MT;
 #ifdef LG_FR_STAMPS
-    unsigned long long fr_[6] = {0, 0, 0, 0, 0, 0}, fr_last_, fr_entry_;
+    unsigned long long fr_[7] = {0, 0, 0, 0, 0, 0, 0}, fr_last_, fr_entry_;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fr_entry_)::"memory");
     fr_last_ = fr_entry_;
 #endif
@@ -1495,6 +1495,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
             xf = xn;
             __builtin_amdgcn_sched_barrier(0);
         }
+        FR_SEG(5);  // (the projection's MFMA loop; its epilogue: segment 6)
         // epilogue: fp16(acc + b3) (+ rotary for q, k) into the staging rows, then one 16-B unit a thread
         // (row, unit u: channels 8 u .. + 7, one head of one part) to its destination
 #pragma unroll
@@ -1535,12 +1536,12 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
     }
 #ifdef LG_FR_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    FR_SEG(5);
-    if (lane == 0 && blockIdx.x < 256) {
+    FR_SEG(6);
+    if (lane == 0 && blockIdx.x < 256) {  // (slot 6: the phase-3 epilogue, not the entry time)
         unsigned long long* d = g_fr_stamps + ((size_t)blockIdx.x * 8 + wave) * 8;
         for (int i = 0; i < 5; ++i) d[i] = fr_[i];
         d[5] = fr_last_ - fr_entry_;
-        d[6] = fr_entry_;
+        d[6] = fr_[6];
         d[7] = fr_[5];
     }
 #endif

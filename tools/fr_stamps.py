@@ -63,13 +63,16 @@ def main():
         if rep:
             rows.append(a)
     a = np.concatenate(rows, 0)
+    if rows16:  # (ffn_rows16_kernel: slot 6 is the phase-3 epilogue; slot 7 its MFMA loop)
+        names = names[:6] + ["phase3_epilogue", "phase3_mfma"]
     out = {"P": P, "n": n, "M": M, "kind": kind, "kernel": "ffn_rows16" if rows16 else "ffn_rows", "workgroups": wgs,
            "median_cycles": {k: float(np.median(a[:, :, i])) for i, k in enumerate(names) if k != "entry"},
            "max_total": float(a[:, :, 5].max()),
-           "entry_spread_cycles": float(np.median(a[:, :, 6].max(1) - a[:, :, 6].min(1)))}
-    last = rows[-1]
-    ent = last[:, :, 6]
-    out["launch_entry_spread_cycles"] = float(ent.max() - ent.min())
+           **({} if rows16 else {"entry_spread_cycles": float(np.median(a[:, :, 6].max(1) - a[:, :, 6].min(1)))})}
+    if not rows16:
+        last = rows[-1]
+        ent = last[:, :, 6]
+        out["launch_entry_spread_cycles"] = float(ent.max() - ent.min())
     print(json.dumps(out), flush=True)
 
 

@@ -36,12 +36,13 @@ for step in "$@"; do
                 python -u tools/fr_stamps.py $arg || exit $?
             grep '^{' "$O/frstamps_${arg// /_}.log" >> "$O/stamps.jsonl" ;;
         smoke)  run 300 smoke.log python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
-        prof_fwd)  # kernel trace of P x n forwards (graph replays), then one forward's timeline
-            P=${arg%x*}; n=${arg#*x}; R=$PWD
-            (cd /tmp && TMPDIR=/tmp run 300 "prof_fwd_${P}x${n}.log" rocprofv3 --kernel-trace --output-format csv \
-                -d "$O/fwd_${P}x${n}" -o m -- python3 "$R/tools/matcher_profile.py" "$P" "$n" 10) || exit $?
-            f=$(find "$O/fwd_${P}x${n}" -name "m_kernel_trace.csv" | head -1)
-            python3 tools/forward_timeline.py "$f" > "$O/timeline_${P}x${n}.txt" 2>&1; cat "$O/timeline_${P}x${n}.txt" | head -20 ;;
+        prof_fwd)  # kernel trace of P x n forwards (graph replays), then one forward's timeline (arg PxN[:fp32])
+            sz=${arg%%:*}; dt=fp16; [ "$sz" != "$arg" ] && dt=${arg#*:}
+            P=${sz%x*}; n=${sz#*x}; R=$PWD; t=${P}x${n}${dt/fp16/}
+            (cd /tmp && TMPDIR=/tmp run 300 "prof_fwd_${t}.log" rocprofv3 --kernel-trace --output-format csv \
+                -d "$O/fwd_${t}" -o m -- python3 "$R/tools/matcher_profile.py" "$P" "$n" 10 "$dt") || exit $?
+            f=$(find "$O/fwd_${t}" -name "m_kernel_trace.csv" | head -1)
+            python3 tools/forward_timeline.py "$f" > "$O/timeline_${t}.txt" 2>&1; cat "$O/timeline_${t}.txt" | head -20 ;;
         pmc_ffn)  # counter passes over lg_linear_cat_ffn at P x n (arg P:n:mode)
             IFS=: read -r P n mode <<< "$arg"; R=$PWD
             for pass in "A:SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA" \
