@@ -921,8 +921,9 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
     static_assert(MB == 1 || 8 * MT * kSP <= kH, "staging over h");
     // phase 3's vectors, loaded with A: b3 [32 NB3 8] fp16 and (E3_QKV) this tile's rows of cos / sin
     constexpr int kB3 = kRed + 2 * MT * 8 * 4;
-    constexpr int kCS = kB3 + NB3 * 256 * 2;           // [2][MT][64] fp16
-    constexpr int kEnd = kCS + (E3 == E3_QKV ? 2 * MT * kD * 2 : 0);
+    constexpr int kCS = kB3 + NB3 * 256 * 2;           // [2][MT] rows of 64 fp16, 144-B pitch (36 banks
+    constexpr int kCSP = 144;                          // a row apart: a column read by 32 rows 2-way, where
+    constexpr int kEnd = kCS + (E3 == E3_QKV ? 2 * MT * kCSP : 0);  // a 128-B pitch was 16-way)
     static_assert(kEnd <= 160 * 1024, "LDS");
     __shared__ __attribute__((aligned(16))) char smem[kEnd];
     lds_char* const lds = (lds_char*)smem;
@@ -1003,7 +1004,12 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
     if (tid < 224) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
 #pragma unroll
     for (int i = 0; i < NV3T; ++i)
-        if (i * 512 + tid < NV3) *(lds_f16x8*)(lds + kB3 + (i * 512 + tid) * 16) = v3[i];
+        if (i * 512 + tid < NB3 * 256 * 2 / 16) {
+            *(lds_f16x8*)(lds + kB3 + (i * 512 + tid) * 16) = v3[i];
+        } else if (i * 512 + tid < NV3) {  // cos / sin unit (table t, row rw, unit cu % 8), padded rows
+            const int cu = i * 512 + tid - NB3 * 256 * 2 / 16;
+            *(lds_f16x8*)(lds + kCS + (cu / 8) * kCSP + (cu % 8) * 16) = v3[i];
+        }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     FR_SEG(0);
@@ -1215,8 +1221,8 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
                     if constexpr (E3 == E3_QKV) {
                         if (cb < 2 * NO) {  // q, k: rotary pairs (d, d + 1) from this row's tables
                             const int rw = 32 * mb + r;  // (tile row; rows past m hold row m - 1's tables)
-                            const f16x4 cc = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + (rw * kD + c % kD) * 2);
-                            const f16x4 ss = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + ((MT + rw) * kD + c % kD) * 2);
+                            const f16x4 cc = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + rw * kCSP + (c % kD) * 2);
+                            const f16x4 ss = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + (MT + rw) * kCSP + (c % kD) * 2);
 #pragma unroll
                             for (int t = 0; t < 4; t += 2) rot_pair(v, t, cc[t], ss[t], cc[t + 1], ss[t + 1]);
                         }
@@ -1293,8 +1299,10 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
     constexpr int kPar = kS3 + MT * U3 * 16;       // b1, gamma, beta [512], b2 [256] fp16
     constexpr int kRed = kPar + (3 * K + NO) * 2;  // row partials [2][16][8 waves] fp32
     constexpr int kB3 = kRed + 2 * MT * 8 * 4;     // b3 [n3] fp16
-    constexpr int kCS = kB3 + NB3 * 256 * 2;       // E3_QKV: cos / sin rows [2][16][64] fp16
-    constexpr int kEnd = kCS + (E3 == E3_QKV ? 2 * MT * kD * 2 : 0);
+    constexpr int kCS = kB3 + NB3 * 256 * 2;       // E3_QKV: cos / sin rows [2][16] fp16, 144-B pitch
+    constexpr int kCSP = 144;                      // (36 banks a row apart: a column read by 16 rows is
+                                                   // conflict-free, where a 128-B pitch was 8-way)
+    constexpr int kEnd = kCS + (E3 == E3_QKV ? 2 * MT * kCSP : 0);
     static_assert(D >= 1 && D <= 16 && (E3 == E3_NONE) == (NB3 == 0) && kEnd <= 160 * 1024, "shape");
     __shared__ __attribute__((aligned(16))) char smem[kEnd];
     lds_char* const lds = (lds_char*)smem;
@@ -1365,7 +1373,12 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         *(lds_f16x8*)(lds + kA + tile_unit(f >> 6, f & 63)) = av[i];
     }
     if (tid < 224) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
-    if (tid < NV3) *(lds_f16x8*)(lds + kB3 + tid * 16) = v3;
+    if (tid < NVB) {
+        *(lds_f16x8*)(lds + kB3 + tid * 16) = v3;
+    } else if (tid < NV3) {  // cos / sin unit (table t, row rw, unit cu % 8) into its padded row
+        const int cu = tid - NVB;
+        *(lds_f16x8*)(lds + kCS + (cu / 8) * kCSP + (cu % 8) * 16) = v3;
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     FR_SEG(0);
@@ -1482,6 +1495,17 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // x' complete
         // ---- phase 3: the wave's NB blocks of 16 output channels, c = 16 (NB w + b) + 4 q + t ----
+        // (E3_QKV: this lane's rotary factors read here, their LDS latency under the MFMAs; the v
+        // blocks read a harmless column too)
+        f16x4 rc[E3 == E3_QKV ? NB : 1], rs[E3 == E3_QKV ? NB : 1];
+        if constexpr (E3 == E3_QKV) {
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const int d = (16 * (NB * wave + b) + 4 * q) % kD;
+                rc[b] = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + r * kCSP + d * 2);
+                rs[b] = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + (MT + r) * kCSP + d * 2);
+            }
+        }
         f32x4 a3[NB] = {};
         f16x8 xf = *(lds_f16x8*)(lds + kX + x_unit(r, q));
 #pragma unroll
@@ -1504,33 +1528,50 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
             const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kB3 + c * 2);
             f16x4 v = f16x4{lin_val(a3[b][0], b4[0]), lin_val(a3[b][1], b4[1]), lin_val(a3[b][2], b4[2]),
                             lin_val(a3[b][3], b4[3])};
-            if constexpr (E3 == E3_QKV) {
+#ifndef LG_FR_ABL
+            constexpr int kAbl = 0;
+#else
+            constexpr int kAbl = LG_FR_ABL;  // diagnostic builds: 1 no rotary, 2 no phase-3 stores
+#endif
+            if constexpr (E3 == E3_QKV && kAbl != 1) {
                 if (c < 2 * NO) {  // q, k: rotary pairs (d, d + 1) from this row's tables
-                    const f16x4 cc = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + (r * kD + c % kD) * 2);
-                    const f16x4 ss = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + ((MT + r) * kD + c % kD) * 2);
 #pragma unroll
-                    for (int t = 0; t < 4; t += 2) rot_pair(v, t, cc[t], ss[t], cc[t + 1], ss[t + 1]);
+                    for (int t = 0; t < 4; t += 2) rot_pair(v, t, rc[b][t], rs[b][t], rc[b][t + 1], rs[b][t + 1]);
                 }
             }
             *(__attribute__((address_space(3))) f16x4*)(lds + kS3 + r * (U3 * 16) + (((c >> 3) ^ r) << 4) + 8 * (q & 1)) = v;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-#pragma unroll
-        for (int i = 0; i < (MT * U3 + 511) / 512; ++i) {
-            const int f = 512 * i + tid, row = f / U3, u = f % U3;
-            if (f < MT * U3 && m0 + row < p.m) {
-                const f16x8 v = *(lds_f16x8*)(lds + kS3 + row * (U3 * 16) + ((u ^ row) << 4));
-                const int c = 8 * u, grow = m0 + row;
-                f16* dst;
+        {  // thread -> row tid / 32, units t + 32 j (t = tid % 32): part j, head t / 8 — one row
+           // lookup per thread, and 32 consecutive threads write a row's 512 B of one part
+            const int row = tid >> 5, t = tid & 31, grow = m0 + row;
+            if (grow < p.m) {
                 if constexpr (E3 == E3_PLAIN) {
-                    dst = c < q3.n_store ? q3.out[0] + (size_t)grow * q3.n_store + c : nullptr;
+#pragma unroll
+                    for (int j = 0; j < U3 / 32; ++j) {
+                        const int u = t + 32 * j;
+#ifdef LG_FR_ABL
+                        if (LG_FR_ABL == 2) continue;
+#endif
+                        if (8 * u < q3.n_store)
+                            *reinterpret_cast<f16x8*>(q3.out[0] + (size_t)grow * q3.n_store + 8 * u) =
+                                *(lds_f16x8*)(lds + kS3 + row * (U3 * 16) + ((u ^ row) << 4));
+                    }
                 } else {
-                    const int part = c / NO, h = (c % NO) / kD;
-                    const LinRow lr = lin_row(p, grow, h);
-                    dst = q3.out[E3 == E3_QKV ? (lr.first ? 0 : 3) + part : (lr.first ? 0 : 1) + 2 * part] + lr.off + c % kD;
+                    const LinRow lr = lin_row(p, grow, t >> 3);
+                    const size_t off = lr.off + (8 * t) % kD;
+#pragma unroll
+                    for (int j = 0; j < U3 / 32; ++j) {
+                        const int u = t + 32 * j;
+                        const f16x8 v = *(lds_f16x8*)(lds + kS3 + row * (U3 * 16) + ((u ^ row) << 4));
+                        f16* const dst = q3.out[E3 == E3_QKV ? (lr.first ? 0 : 3) + j : (lr.first ? 0 : 1) + 2 * j] + off;
+#ifdef LG_FR_ABL
+                        if (LG_FR_ABL == 2) continue;
+#endif
+                        *reinterpret_cast<f16x8*>(dst) = v;
+                    }
                 }
-                if (dst) *reinterpret_cast<f16x8*>(dst) = v;
             }
         }
     }

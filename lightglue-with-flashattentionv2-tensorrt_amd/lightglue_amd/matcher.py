@@ -664,16 +664,18 @@ class LightGlueMatcher(nn.Module):
     # 0.496 / 0.481 / 0.494 / 0.480 / 0.492, P = 4 0.790 / 0.729 / 0.747 / 0.723 / 0.772, P = 16 2.165 /
     # 2.133 / 2.163 / 2.128 / 2.183: "sh" with the 32-row FFN kernel; folding Wqkv (768 channels, 384 KiB
     # more per workgroup's stream) cost the launch more than the separate projection took. With the
-    # 16-row kernel (2,048..4,096 rows: twice the workgroups) "sqh" wins (profiles/r06/chain_kinds_rows16_ab
-    # .jsonl, sh / sqh: P = 1 n = 1024 0.445 / 0.439, n = 2048 0.707 / 0.673, P = 2 0.588 / 0.558; n = 512
-    # 0.375 / 0.383, P = 4 0.767 / 0.765). Outputs bitwise equal in every form. LG_CHAIN (or this
+    # 16-row kernel (up to 4,096 rows: twice the workgroups) and the QKV epilogues' rotary factors read
+    # from a conflict-free table (prefetched, in the 16-row kernel), "sqh" wins at every size
+    # (profiles/r06/chain_kinds_rows16_ab.jsonl, chain_kinds_sqh_ab.jsonl; sh / sqh: P = 1 n = 512 0.372 /
+    # 0.367, n = 1024 0.440 / 0.420, n = 2048 0.679 / 0.634, P = 2 0.560 / 0.513, P = 4 0.724 / 0.709,
+    # P = 8 1.195 / 1.159, P = 16 2.140 / 2.124). Outputs bitwise equal in every form. LG_CHAIN (or this
     # attribute) overrides, for A/B.
     chain_kinds: Optional[str] = None
 
     def _chain_kinds(self, rows: int) -> str:
         if self.chain_kinds is not None:
             return self.chain_kinds
-        return os.environ.get("LG_CHAIN", "sqh" if 2048 <= rows <= 4096 else "sh")
+        return os.environ.get("LG_CHAIN", "sqh")
 
     def chain_ok(self, x: torch.Tensor, m: int, n: int) -> bool:
         """The chained fp16 path: every block fusable (4 x 64 heads, d = 256) and the fp16 head."""
@@ -683,10 +685,10 @@ class LightGlueMatcher(nn.Module):
     def _forward_chain(self, x, cos, sin, splits):
         """fp16 hip path with the layers chained (round 6): FFN launches also project their output for
         the attention that follows (lg_linear_cat_ffn_proj) — by default the self block's FFN the cross
-        block's to_qk | to_v and the last FFN the assignment head's [W_final / scale ; w_match]
-        (chain_kinds) — so a layer is 5 launches (Wqkv, self attention, FFN + cross projection, cross
-        attention, FFN) and a forward 1 + 5 L + 3 (inputs, the layers, the head's similarity, logsumexp
-        close and combine; lightglue.py:328-353)."""
+        block's to_qk | to_v, the cross block's FFN the next layer's Wqkv (+ rotary) and the last FFN
+        the assignment head's [W_final / scale ; w_match] (chain_kinds) — so a layer is 4 launches (self
+        attention, FFN + cross projection, cross attention, FFN + next projection) and a forward
+        2 + 4 L + 2 (inputs, layer 0's Wqkv, the layers, the head's two; lightglue.py:328-353)."""
         dt = x.dtype
         m, n, pr = _sp(splits)
         kinds = self._chain_kinds(x.shape[1])
