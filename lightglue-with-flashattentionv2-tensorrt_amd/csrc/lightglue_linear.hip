@@ -161,6 +161,31 @@ __device__ __forceinline__ float mixf(float x, unsigned g2, unsigned b2) {
     else asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(r) : "v"(x), "v"(g2), "v"(b2));
     return r;
 }
+// The packed forms (round 6): h2 = (fp16(acc0 + b.lo), fp16(acc1 + b.hi)) in one register, each half
+// rounded once as mixh does; mixn(h2, a, c) = h2's HI-th half * a + c in fp32 (the LayerNorm's
+// normalisation read straight from the packed fp16 values)
+__device__ __forceinline__ unsigned mixh2(float acc0, float acc1, unsigned b2) {
+    unsigned h;
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, %2 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %0, %3, 1.0, %2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(h)
+        : "v"(acc0), "v"(b2), "v"(acc1));
+    return h;
+}
+template <int HI>
+__device__ __forceinline__ float mixn(unsigned h2, float a, float c) {
+    float r;
+    if constexpr (HI) asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h2), "v"(a), "v"(c));
+    else asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h2), "v"(a), "v"(c));
+    return r;
+}
+// the row sums of one packed pair: s1 += h.lo + h.hi, s2 += h.lo^2 + h.hi^2 (v_dot2_f32_f16: the f16
+// products exact in fp32)
+__device__ __forceinline__ void row_sums2(unsigned h2, float& s1, float& s2) {
+    const f16x2 h = __builtin_bit_cast(f16x2, h2);
+    s1 = __builtin_amdgcn_fdot2(h, f16x2{(f16)1.f, (f16)1.f}, s1, false);
+    s2 = __builtin_amdgcn_fdot2(h, h, s2, false);
+}
 template <int HI>
 __device__ __forceinline__ float mixh(float acc, unsigned b2) {
     unsigned h;
@@ -884,6 +909,17 @@ struct Proj3 {
     f16* out[6];        // SPLIT2: a0 a1 b0 b1; QKV: q0 k0 v0 q1 k1 v1 (per-image head-major); PLAIN: [m, n_store]
     int n_store;        // E3_PLAIN: channels stored per row (the first n_store of 32 NB3 8)
 };
+// The weight stream's wave sync (A/B, -DLG_FFN_SYNC=<pieces>): a workgroup barrier every that many
+// 1-KiB pieces per wave inside each phase, so that no wave runs ahead of the others' streams.
+#ifndef LG_FFN_SYNC
+#define LG_FFN_SYNC 0
+#endif
+#define FFN_SYNC(pieces_done, pieces_total)                                                   \
+    do {                                                                                      \
+        if constexpr (LG_FFN_SYNC > 0) {                                                      \
+            if ((pieces_done) % LG_FFN_SYNC == 0 && (pieces_done) < (pieces_total)) __builtin_amdgcn_s_barrier(); \
+        }                                                                                     \
+    } while (0)
 // Diagnostic build (-DLG_FR_STAMPS, tools/fr_stamps.py; never shipped): per wave of the first 256
 // workgroups, s_memtime cycles of chained segments (0 entry -> A in LDS, 1 phase 1, 2 LayerNorm + GELU,
 // 3 phase 2, 4 epilogue), read back by lg_diag_fr_stamps.
@@ -1042,6 +1078,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
         }
         af = an;
         __builtin_amdgcn_sched_barrier(0);
+        FFN_SYNC(2 * (j + 1), 2 * NS1);
     }
 
     FR_SEG(1);
@@ -1053,6 +1090,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
     // exchange through LDS (vector issue bounds this phase: ~19 VALU per value, two waves a SIMD)
     float* const red = (float*)(void*)(smem + kRed);  // [pass][row][wave]
     float sm[MB], sq[MB];
+    unsigned hp[2][MB][8];  // h as packed fp16 pairs: block b, rows mb, (g, pair u) at 2 g + u
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
         float s1 = 0.f, s2 = 0.f;
@@ -1062,11 +1100,9 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
             for (int g = 0; g < 4; ++g) {
                 const u32x2 b4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + (64 * wave + 32 * b + 8 * g + 4 * hh) * 2);
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const float h = (t & 1) ? mixh<1>(acc[b][mb][4 * g + t], b4[t >> 1]) : mixh<0>(acc[b][mb][4 * g + t], b4[t >> 1]);
-                    acc[b][mb][4 * g + t] = h;
-                    s1 += h;
-                    s2 = __builtin_fmaf(h, h, s2);
+                for (int u = 0; u < 2; ++u) {
+                    hp[b][mb][2 * g + u] = mixh2(acc[b][mb][4 * g + 2 * u], acc[b][mb][4 * g + 2 * u + 1], b4[u]);
+                    row_sums2(hp[b][mb][2 * g + u], s1, s2);
                 }
             }
         sm[mb] = s1 + __shfl_xor(s1, 32, 64);
@@ -1102,11 +1138,12 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
                 const u32x2 be4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + 2 * K * 2 + n * 2);
                 f16x4 o;
 #pragma unroll
-                for (int u = 0; u < 4; u += 2) {
-                    const f32x2 xr = f32x2{acc[b][mb][4 * g + u], acc[b][mb][4 * g + u + 1]} * rstd + nmr;
-                    const f32x2 gl = gelu_as2(f32x2{mixf<0>(xr[0], g4[u >> 1], be4[u >> 1]), mixf<1>(xr[1], g4[u >> 1], be4[u >> 1])});
-                    o[u] = (f16)gl[0];
-                    o[u + 1] = (f16)gl[1];
+                for (int u = 0; u < 2; ++u) {
+                    const unsigned h2 = hp[b][mb][2 * g + u];
+                    const float x0 = mixn<0>(h2, rstd, nmr), x1 = mixn<1>(h2, rstd, nmr);
+                    const f32x2 gl = gelu_as2(f32x2{mixf<0>(x0, g4[u], be4[u]), mixf<1>(x1, g4[u], be4[u])});
+                    o[2 * u] = (f16)gl[0];
+                    o[2 * u + 1] = (f16)gl[1];
                 }
                 *(__attribute__((address_space(3))) f16x4*)(lds + kH + row * 1024 + (((8 * wave + 4 * b + g) ^ (row & 15)) << 4) + 8 * hh) = o;
             }
@@ -1126,6 +1163,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
         for (int mb = 0; mb < MB; ++mb) o2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa, hf.v[mb], o2[mb], 0, 0, 0);
         hf = hn;
         __builtin_amdgcn_sched_barrier(0);
+        FFN_SYNC(j + 1 - NS1, NS1);
     }
     FR_SEG(3);
     if constexpr (MB > 1) {  // (the staging rows lie over h: every wave done reading it)
@@ -1203,6 +1241,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
                 for (int mb = 0; mb < MB; ++mb) a3[b][mb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w3[b], xf.v[mb], a3[b][mb], 0, 0, 0);
             xf = xn;
             __builtin_amdgcn_sched_barrier(0);
+            FFN_SYNC(NB3 * (j + 1), NB3 * NS3);
         }
         // epilogue: fp16(acc + b3) (+ rotary for q, k) as the standalone projections compute it, the
         // wave's rows x 32 channels of a block staged (its own rows of the staging region), then two
@@ -1396,6 +1435,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w4[b], bf, acc[b], 0, 0, 0);
         bf = bn;
         __builtin_amdgcn_sched_barrier(0);
+        FFN_SYNC(4 * (s + 1), 64);
     }
     FR_SEG(1);
 
@@ -1403,21 +1443,25 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
     // one rounding, the row's sum and sum of squares over the 4 q lanes, then the 8 waves via LDS ----
     float* const red = (float*)(void*)(smem + kRed);
     float s1 = 0.f, s2 = 0.f;
+    unsigned hp[4][2];  // h as packed fp16 pairs: block b, channels 4 q + 2 u, + 1
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
         const u32x2 b4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + (64 * wave + 16 * b + 4 * q) * 2);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const float h = (t & 1) ? mixh<1>(acc[b][t], b4[t >> 1]) : mixh<0>(acc[b][t], b4[t >> 1]);
-            acc[b][t] = h;
-            s1 += h;
-            s2 = __builtin_fmaf(h, h, s2);
+        for (int u = 0; u < 2; ++u) {
+            hp[b][u] = mixh2(acc[b][2 * u], acc[b][2 * u + 1], b4[u]);
+            row_sums2(hp[b][u], s1, s2);
         }
     }
-    s1 += __shfl_xor(s1, 16, 64);
-    s2 += __shfl_xor(s2, 16, 64);
-    s1 += __shfl_xor(s1, 32, 64);
-    s2 += __shfl_xor(s2, 32, 64);
+    // over the row's 4 lanes (l, l ^ 16, l ^ 32, l ^ 48) by lane-group swaps (VALU, no LDS trip)
+    auto xsum = [](float x) {
+        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+        const float y = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+        const auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(y), __float_as_uint(y), false, false);
+        return __uint_as_float(c[0]) + __uint_as_float(c[1]);
+    };
+    s1 = xsum(s1);
+    s2 = xsum(s2);
     if (q == 0) {
         red[r * 8 + wave] = s1;
         red[MT * 8 + r * 8 + wave] = s2;
@@ -1440,11 +1484,11 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
             const u32x2 be4 = *(__attribute__((address_space(3))) u32x2*)(lds + kPar + 2 * K * 2 + n * 2);
             f16x4 o;
 #pragma unroll
-            for (int u = 0; u < 4; u += 2) {
-                const f32x2 xr = f32x2{acc[b][u], acc[b][u + 1]} * rstd + nmr;
-                const f32x2 gl = gelu_as2(f32x2{mixf<0>(xr[0], g4[u >> 1], be4[u >> 1]), mixf<1>(xr[1], g4[u >> 1], be4[u >> 1])});
-                o[u] = (f16)gl[0];
-                o[u + 1] = (f16)gl[1];
+            for (int u = 0; u < 2; ++u) {
+                const float x0 = mixn<0>(hp[b][u], rstd, nmr), x1 = mixn<1>(hp[b][u], rstd, nmr);
+                const f32x2 gl = gelu_as2(f32x2{mixf<0>(x0, g4[u], be4[u]), mixf<1>(x1, g4[u], be4[u])});
+                o[2 * u] = (f16)gl[0];
+                o[2 * u + 1] = (f16)gl[1];
             }
             *(__attribute__((address_space(3))) f16x4*)(lds + kH + tile_unit(r, n >> 3) + 8 * (q & 1)) = o;
         }
@@ -1464,6 +1508,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         o2[1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wb, hf, o2[1], 0, 0, 0);
         hf = hn;
         __builtin_amdgcn_sched_barrier(0);
+        FFN_SYNC(2 * (s + 1), 32);
     }
     FR_SEG(3);
     // ---- out = fp16(fp16(acc + b2) + x): fp16(acc + b2) into the x' tile, then one 16-B unit a thread
@@ -1518,6 +1563,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
             for (int b = 0; b < NB; ++b) a3[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w3[b], xf, a3[b], 0, 0, 0);
             xf = xn;
             __builtin_amdgcn_sched_barrier(0);
+            FFN_SYNC(NB * (s + 1), 8 * NB);
         }
         FR_SEG(5);  // (the projection's MFMA loop; its epilogue: segment 6)
         // epilogue: fp16(acc + b3) (+ rotary for q, k) into the staging rows, then one 16-B unit a thread

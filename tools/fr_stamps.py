@@ -69,6 +69,11 @@ def main():
            "median_cycles": {k: float(np.median(a[:, :, i])) for i, k in enumerate(names) if k != "entry"},
            "max_total": float(a[:, :, 5].max()),
            **({} if rows16 else {"entry_spread_cycles": float(np.median(a[:, :, 6].max(1) - a[:, :, 6].min(1)))})}
+    # per workgroup: how far apart its 8 waves finish phase 1 (cumulative prologue + phase 1), the
+    # LayerNorm barrier's wait for the slowest
+    ends = a[:, :, 0] + a[:, :, 1]
+    out["phase1_end_spread_cycles"] = float(np.median(ends.max(1) - ends.min(1)))
+    out["phase1_end_slowest_wave"] = int(np.bincount(ends.argmax(1), minlength=8).argmax())
     if not rows16:
         last = rows[-1]
         ent = last[:, :, 6]
