@@ -910,7 +910,11 @@ struct Proj3 {
     int n_store;        // E3_PLAIN: channels stored per row (the first n_store of 32 NB3 8)
 };
 // The weight stream's wave sync (A/B, -DLG_FFN_SYNC=<pieces>): a workgroup barrier every that many
-// 1-KiB pieces per wave inside each phase, so that no wave runs ahead of the others' streams.
+// 1-KiB pieces per wave inside each phase, so that no wave runs ahead of the others' streams. The
+// waves of a workgroup finish phase 1 ~3.8 k cycles apart (stamps: the LayerNorm's first barrier
+// waits for the slowest); with a barrier every 8 pieces 0.5 k apart, but phase 1 itself takes that
+// much longer: the CU's stream is bandwidth-bound either way (P = 1 / 4 / 16 FFN 10.0 / 14.6 / 46.0
+// us shipped, 10.1 / 15.1 / 46.4 with 8; forwards equal; profiles/r06/ffn_wave_sync_ab.jsonl). Off.
 #ifndef LG_FFN_SYNC
 #define LG_FFN_SYNC 0
 #endif
