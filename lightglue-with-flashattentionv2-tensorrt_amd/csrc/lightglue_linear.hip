@@ -26,6 +26,7 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <cstdlib>
 
 #include "lightglue_glue.h"
 #include "mha_hd64.h"
@@ -1325,7 +1326,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
 // (64 + 2 s + b), phase 3 W3[16 (2 NB3 w + b) + i][32 s + 8 q ..] (96 + 2 NB3 s + b): the same channel
 // sets per wave as the 32-row layout, so the rounding and order of every sum are unchanged but for
 // the k order inside an MFMA.
-template <int D, int E3, int NB3>
+template <int D, int E3, int NB3, int SP = 1>
 __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16* __restrict__ gamma,
                                                             const f16* __restrict__ beta, float eps,
                                                             const f16* __restrict__ wp, const f16* __restrict__ b2,
@@ -1334,6 +1335,8 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
     constexpr int NP = 96 + NB3 * 16;              // the wave's stream: pieces of 1 KiB
     constexpr int R = 2 * D;                       // pieces in flight (a register ring)
     constexpr int NB = 2 * NB3;                    // phase 3: 16-channel blocks per wave
+    constexpr int NBP = NB / (SP > 1 ? SP : 1);    // ... of them this workgroup's (SP parts of a tile)
+    constexpr int NPS = 96 + 8 * NBP;              // the pieces this workgroup's waves consume
     constexpr int U3 = 32 * NB3;                   // phase 3: 16-B units per output row
     constexpr int kA = 0;                          // A tile [16][1 KiB]: x units 0..31, heads 32..63
     constexpr int kH = kA + MT * 1024;             // h tile [16][1 KiB]
@@ -1347,12 +1350,16 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
                                                    // conflict-free, where a 128-B pitch was 8-way)
     constexpr int kEnd = kCS + (E3 == E3_QKV ? 2 * MT * kCSP : 0);
     static_assert(D >= 1 && D <= 16 && (E3 == E3_NONE) == (NB3 == 0) && kEnd <= 160 * 1024, "shape");
+    static_assert(SP == 1 || (E3 != E3_NONE && NB % SP == 0), "parts");
     __shared__ __attribute__((aligned(16))) char smem[kEnd];
     lds_char* const lds = (lds_char*)smem;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 15, q = lane >> 4;
-    const int m0 = blockIdx.x * MT;
+    // SP > 1: SP workgroups per 16-row tile, each running phases 1 and 2 whole and 1/SP of phase 3
+    // (at a few hundred tiles the chip has the CUs; the projection's weight stream and epilogue halve)
+    const int part = SP > 1 ? (int)blockIdx.x % SP : 0;
+    const int m0 = (SP > 1 ? (int)blockIdx.x / SP : (int)blockIdx.x) * MT;
 #ifdef LG_FR_STAMPS
     unsigned long long fr_[7] = {0, 0, 0, 0, 0, 0, 0}, fr_last_, fr_entry_;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fr_entry_)::"memory");
@@ -1398,7 +1405,12 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
 
     const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(wp), (short)0, 8 * NP * 1024, 0x00020000);
     const unsigned wo = (unsigned)(wave * NP * 1024 + lane * 16);
-    auto piece = [&](int i) { return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, wo, i * 1024, 0)); };
+    // stream position i -> packed piece (phase 3: this part's NBP blocks of each k32 step)
+    const int p3off = __builtin_amdgcn_readfirstlane(part * NBP * 1024);
+    auto piece = [&](int i) {
+        const int so = i < 96 ? i * 1024 : (96 + NB * ((i - 96) / NBP) + (i - 96) % NBP) * 1024 + p3off;
+        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, wo, so, 0));
+    };
     f16x8 w_[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
@@ -1407,7 +1419,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
     }
     auto take = [&](int i) {
         const f16x8 w = w_[i % R];
-        if (i + R < NP) w_[i % R] = piece(i + R);
+        if (i + R < NPS) w_[i % R] = piece(i + R);
         return w;
     };
 #pragma unroll
@@ -1533,7 +1545,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         const f16x8 xr = *(lds_f16x8*)(lds + kA + tile_unit(row, u));
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = res_add(v[e], xr[e]);
-        if (m0 + row < p.m) *reinterpret_cast<f16x8*>(p.out[0] + (size_t)(m0 + row) * NO + 8 * u) = v;
+        if (part == 0 && m0 + row < p.m) *reinterpret_cast<f16x8*>(p.out[0] + (size_t)(m0 + row) * NO + 8 * u) = v;
         if constexpr (E3 != E3_NONE) *(lds_f16x8*)(lds + kX + x_unit(row, u)) = v;
     }
 #ifdef LG_FR_STAMPS
@@ -1546,35 +1558,35 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         // ---- phase 3: the wave's NB blocks of 16 output channels, c = 16 (NB w + b) + 4 q + t ----
         // (E3_QKV: this lane's rotary factors read here, their LDS latency under the MFMAs; the v
         // blocks read a harmless column too)
-        f16x4 rc[E3 == E3_QKV ? NB : 1], rs[E3 == E3_QKV ? NB : 1];
+        f16x4 rc[E3 == E3_QKV ? NBP : 1], rs[E3 == E3_QKV ? NBP : 1];
         if constexpr (E3 == E3_QKV) {
 #pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                const int d = (16 * (NB * wave + b) + 4 * q) % kD;
+            for (int b = 0; b < NBP; ++b) {
+                const int d = (16 * (NB * wave + part * NBP + b) + 4 * q) % kD;
                 rc[b] = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + r * kCSP + d * 2);
                 rs[b] = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + (MT + r) * kCSP + d * 2);
             }
         }
-        f32x4 a3[NB] = {};
+        f32x4 a3[NBP] = {};
         f16x8 xf = *(lds_f16x8*)(lds + kX + x_unit(r, q));
 #pragma unroll
         for (int s = 0; s < 8; ++s) {
-            f16x8 w3[NB];
+            f16x8 w3[NBP];
 #pragma unroll
-            for (int b = 0; b < NB; ++b) w3[b] = take(96 + NB * s + b);
+            for (int b = 0; b < NBP; ++b) w3[b] = take(96 + NBP * s + b);
             const f16x8 xn = s + 1 < 8 ? *(lds_f16x8*)(lds + kX + x_unit(r, 4 * (s + 1) + q)) : xf;
 #pragma unroll
-            for (int b = 0; b < NB; ++b) a3[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w3[b], xf, a3[b], 0, 0, 0);
+            for (int b = 0; b < NBP; ++b) a3[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w3[b], xf, a3[b], 0, 0, 0);
             xf = xn;
             __builtin_amdgcn_sched_barrier(0);
-            FFN_SYNC(NB * (s + 1), 8 * NB);
+            FFN_SYNC(NBP * (s + 1), 8 * NBP);
         }
         FR_SEG(5);  // (the projection's MFMA loop; its epilogue: segment 6)
         // epilogue: fp16(acc + b3) (+ rotary for q, k) into the staging rows, then one 16-B unit a thread
         // (row, unit u: channels 8 u .. + 7, one head of one part) to its destination
 #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            const int c = 16 * (NB * wave + b) + 4 * q;
+        for (int b = 0; b < NBP; ++b) {
+            const int c = 16 * (NB * wave + part * NBP + b) + 4 * q;
             const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kB3 + c * 2);
             f16x4 v = f16x4{lin_val(a3[b][0], b4[0]), lin_val(a3[b][1], b4[1]), lin_val(a3[b][2], b4[2]),
                             lin_val(a3[b][3], b4[3])};
@@ -1604,6 +1616,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
 #ifdef LG_FR_ABL
                         if (LG_FR_ABL == 2) continue;
 #endif
+                        if (SP > 1 && ((8 * u) % (16 * NB)) / (16 * NBP) != part) continue;  // (another part's)
                         if (8 * u < q3.n_store)
                             *reinterpret_cast<f16x8*>(q3.out[0] + (size_t)grow * q3.n_store + 8 * u) =
                                 *(lds_f16x8*)(lds + kS3 + row * (U3 * 16) + ((u ^ row) << 4));
@@ -1614,6 +1627,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
 #pragma unroll
                     for (int j = 0; j < U3 / 32; ++j) {
                         const int u = t + 32 * j;
+                        if (SP > 1 && ((8 * u) % (16 * NB)) / (16 * NBP) != part) continue;  // (another part's)
                         const f16x8 v = *(lds_f16x8*)(lds + kS3 + row * (U3 * 16) + ((u ^ row) << 4));
                         f16* const dst = q3.out[E3 == E3_QKV ? (lr.first ? 0 : 3) + j : (lr.first ? 0 : 1) + 2 * j] + off;
 #ifdef LG_FR_ABL
@@ -2018,14 +2032,32 @@ int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
 // 32-row kernel two workgroups per CU (128 VGPRs, an 8-piece ring, staging over h), for one workgroup's
 // A-tile latency under the other's stream — 46.0 -> 47.1 us at 32,768 rows, 23.0 -> 24.1 at 16,384,
 // equal bits; profiles/r06/ffn_rows_occ2_ab.jsonl.)
+// The 16-row kernel's projection split over two workgroups per tile (ffn_rows16_kernel<…, SP = 2>):
+// 2 when that is at most 128 tiles (LG_FFN_SPLIT=0: never, =2: while 2 x tiles fill at most one round)
+int ffn_split_parts(int tiles) {
+    static const int env = [] {
+        const char* e = std::getenv("LG_FFN_SPLIT");
+        return e ? std::atoi(e) : -1;
+    }();
+    if (env == 0) return 1;
+    return (env == 2 ? 2 * tiles <= kTileGrid : tiles <= 64) ? 2 : 1;
+}
 template <int E3, int NB3>
 void launch_ffn_rows(const LinArgs& p, const f16* gamma, const f16* beta, float eps, const f16* wp, const f16* b2,
                      const Proj3& q3, hipStream_t stream) {
     const int mode = g_ffn_fused.load();
     if (mode == 3 || (mode != 2 && p.m <= 16 * kTileGrid)) {
         const f16* wp16 = wp + (size_t)8 * (96 + 16 * NB3) * 1024 / 2;
-        hipLaunchKernelGGL((ffn_rows16_kernel<kFrDepth, E3, NB3>), dim3((p.m + 15) / 16), dim3(512), 0, stream, p, gamma, beta,
-                           eps, wp16, b2, q3);
+        const int tiles = (p.m + 15) / 16;
+        if constexpr (E3 != E3_NONE) {
+            if (ffn_split_parts(tiles) == 2) {
+                hipLaunchKernelGGL((ffn_rows16_kernel<kFrDepth, E3, NB3, 2>), dim3(2 * tiles), dim3(512), 0, stream, p,
+                                   gamma, beta, eps, wp16, b2, q3);
+                return;
+            }
+        }
+        hipLaunchKernelGGL((ffn_rows16_kernel<kFrDepth, E3, NB3>), dim3(tiles), dim3(512), 0, stream, p, gamma, beta, eps,
+                           wp16, b2, q3);
     } else if (p.m <= 32 * kTileGrid)
         hipLaunchKernelGGL((ffn_rows_kernel<1, kFrDepth, E3, NB3>), dim3((p.m + 31) / 32), dim3(512), 0, stream, p, gamma, beta,
                            eps, wp, b2, q3);
