@@ -194,11 +194,11 @@ int32_t lg_pair_inputs(const void* desc0, const void* desc1, const void* kpts0, 
                        hipStream_t stream);
 
 /* Test and benchmark hook: the projections' tile forms for launches of many rows (several image
- * pairs per forward): 0 the 64 x 64 form only, 1 the 256 x 128 form where n allows, 2 the
- * 256 x 256 form where n allows (plain bias outputs; else 1), 4 the 128 x 128 form on 4 waves (two
- * workgroups per CU; the by-size choice from 128 of its tiles and 8,192 rows on), -1 (the default)
- * chosen by size; 3 and 5 (round 5's A/B forms, removed) select 1 and 4; values outside -1..5 are
- * clamped. The environment variable LG_LINEAR_WIDE sets the initial mode the same way. Every form
+ * pairs per forward): 0 the 64 x 64 form only, 4 the 128 x 128 form on 4 waves (two workgroups per
+ * CU; the by-size choice from 128 of its tiles and 8,192 rows on), -1 (the default) chosen by size;
+ * 1 the 256 x 128 form and 2 the 256 x 256 form (plain bias outputs; else 1) where n allows — in A/B
+ * builds only (-DLG_LINEAR_AB_FORMS=1, tools/build_linear_variant.sh); the shipped library runs form 4
+ * for them, as for 3 and 5 (round 5's A/B forms, removed); values outside -1..5 are clamped. The environment variable LG_LINEAR_WIDE sets the initial mode the same way. Every form
  * gives the same bits. Returns the previous mode. */
 int32_t lg_linear_set_wide(int32_t mode);
 

@@ -1958,6 +1958,9 @@ bool aligned8(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 7) == 0;
 // P = 32 -1.0 % (form_fwd_ab.jsonl): the default below; forms 1 and 2 (the round's earlier default was
 // form 1 from half a round of its tiles) stay for lg_linear_set_wide / LG_LINEAR_WIDE, which force a
 // form where n and the operand alignment allow.
+#ifndef LG_LINEAR_AB_FORMS
+#define LG_LINEAR_AB_FORMS 0  // 1: forms 1 and 2 built (A/B builds: tools/build_linear_variant.sh); the
+#endif                        // shipped library maps them to form 4 (no kernel that its default never runs)
 int tile_form(const LinArgs& p, int epi, bool gather) {
     bool al = aligned16(p.bias);
     const int nout = epi == EPI_BIAS ? 1 : epi == EPI_QKV_ROTARY ? 6 : 4;
@@ -1976,7 +1979,8 @@ int tile_form(const LinArgs& p, int epi, bool gather) {
     // does not call there. Whole forwards (form_fwd_ab_final.jsonl): P = 2 (4,096 rows) 2 % faster
     // with the 64 x 64 form everywhere, P = 4 / 8 / 16 7 / 3 / 1 % faster than form 1 with this rule)
     (void)gather;
-    const int f = w >= 0 ? w : (p.m >= 8192 && (long)((p.m + 127) / 128) * (p.n / 128) >= 128 ? 4 : 0);
+    int f = w >= 0 ? w : (p.m >= 8192 && (long)((p.m + 127) / 128) * (p.n / 128) >= 128 ? 4 : 0);
+    if (!LG_LINEAR_AB_FORMS && (f == 1 || f == 2 || f == 3)) f = 4;
     if (f == 2 && p.n % 256 == 0) return (p.res || epi != EPI_BIAS) ? 1 : 2;
     if (f >= 4 && p.n % 128 == 0) return 4;  // (5: round 5's 32-deep A/B variant of form 4, removed in round 6)
     return f >= 1 && p.n % 128 == 0 ? 1 : 0;  // (3: round 5's 128 x 256 A/B form, removed in round 6)
@@ -2007,10 +2011,12 @@ int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
     int form = tile_form(p, EPI, GATHER);
     if (GATHER && form == 2) form = 1;  // (the gather's per-piece sources do not fit beside 64 x 128 wave tiles)
     switch (form) {
+#if LG_LINEAR_AB_FORMS
         case 1: launch_tile<EPI, GATHER, 256, 128, 64, 3>(p, stream); break;
         case 2:
             if constexpr (!GATHER && EPI == EPI_BIAS) launch_tile<EPI, GATHER, 256, 256, 32, 4>(p, stream);
             break;
+#endif
         case 4: launch_tile<EPI, GATHER, 128, 128, 64, 2, 4>(p, stream); break;
         default:
             p.mtiles = (p.m + kBM - 1) / kBM;
@@ -2033,7 +2039,10 @@ int32_t launch(LinArgs& p, hipStream_t stream, const char* what) {
 // A-tile latency under the other's stream — 46.0 -> 47.1 us at 32,768 rows, 23.0 -> 24.1 at 16,384,
 // equal bits; profiles/r06/ffn_rows_occ2_ab.jsonl.)
 // The 16-row kernel's projection split over two workgroups per tile (ffn_rows16_kernel<…, SP = 2>):
-// 2 when that is at most 128 tiles (LG_FFN_SPLIT=0: never, =2: while 2 x tiles fill at most one round)
+// up to 64 tiles (LG_FFN_SPLIT=0: never, =2: while 2 x tiles fill at most one round). Measured
+// (profiles/r06/ffn_phase3_split_ab.jsonl, single-pair forwards, ms): n = 512 (64 tiles) 0.368 -> 0.353;
+// n = 1024 (128 tiles) 0.427-0.431 -> 0.434 split, kept whole. Three / four parts (one or two blocks
+// per wave, an A/B build) : n = 512 0.351-0.354 -> 0.355-0.359, n = 256 0.334 -> 0.325.
 int ffn_split_parts(int tiles) {
     static const int env = [] {
         const char* e = std::getenv("LG_FFN_SPLIT");
@@ -2050,7 +2059,8 @@ void launch_ffn_rows(const LinArgs& p, const f16* gamma, const f16* beta, float 
         const f16* wp16 = wp + (size_t)8 * (96 + 16 * NB3) * 1024 / 2;
         const int tiles = (p.m + 15) / 16;
         if constexpr (E3 != E3_NONE) {
-            if (ffn_split_parts(tiles) == 2) {
+            const int sp = ffn_split_parts(tiles);
+            if (sp == 2) {
                 hipLaunchKernelGGL((ffn_rows16_kernel<kFrDepth, E3, NB3, 2>), dim3(2 * tiles), dim3(512), 0, stream, p,
                                    gamma, beta, eps, wp16, b2, q3);
                 return;

@@ -561,9 +561,11 @@ def test_torch_glue_runs_pairs_one_by_one():
 @pytest.mark.parametrize("pairs,n0,n1", [(3, 37, 70), (2, 1000, 777), (16, 1024, 1024), (9, 1000, 1011), (40, 20, 30), (5, 1, 63),
                                          (4, 56, 1)])
 def test_wide_projections_equal_narrow(pairs, n0, n1):
-    """The projections' tile forms (csrc/lightglue_linear.hip linear_tile_kernel: 256 x 128 and
-    256 x 256 tiles on 8 waves, 128 x 128 on 4, with the LDS-staged coalesced epilogue, taken for launches of at
-    least one round of tiles: several image pairs per forward) give the bits of the 64 x 64 form on
+    """The projections' tile forms (csrc/lightglue_linear.hip linear_tile_kernel: 128 x 128 on 4 waves —
+    and, in an A/B build (-DLG_LINEAR_AB_FORMS=1, run the suite with MHA_HD64_LIB=<it>), 256 x 128 and
+    256 x 256 on 8 waves; the shipped library runs form 4 for modes 1 and 2 — with the LDS-staged
+    coalesced epilogue, taken for launches of at least one round of tiles: several image pairs per
+    forward) give the bits of the 64 x 64 form on
     every fused entry point — ragged row counts (rows past m in a tile: computed on the clamped last
     row, their stores rewrite that row's bytes), both K (256 and 512), residual on and off, the
     A-gather of lg_linear_cat, the per-image scatters. The head-major epilogue's row paths: the
