@@ -24,8 +24,10 @@ def family(name):
             if k.startswith("linear") and k != "linear_ln_kernel":
                 return n.split("(")[0]
             if k.startswith("ffn_rows"):  # the phase-3 kind: the E3 template argument (demangled or not)
-                m = re.search(r"ffn_rows(?:16)?_kernel<(?:\d+, )?\d+, (\d+), \d+>", n) or \
-                    re.search(r"ffn_rows(?:16)?_kernelI(?:Li\d+E)?Li\d+ELi(\d+)ELi\d+E", n)
+                if k == "ffn_rows16_kernel":  # <D, E3, NB3(, SP)>
+                    m = re.search(r"ffn_rows16_kernel<\d+, (\d+),", n) or re.search(r"ffn_rows16_kernelILi\d+ELi(\d+)E", n)
+                else:  # <MB, D, E3, NB3>
+                    m = re.search(r"ffn_rows_kernel<\d+, \d+, (\d+),", n) or re.search(r"ffn_rows_kernelILi\d+ELi\d+ELi(\d+)E", n)
                 return k + (E3_NAMES.get(m.group(1), "") if m else "")
             return k
     return "FW " + n.split("(")[0][:60]
