@@ -1262,7 +1262,12 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
                     const f16x4 b4 = *(__attribute__((address_space(3))) f16x4*)(lds + kB3 + c * 2);
                     f16x4 v = f16x4{lin_val(a3[b][mb][4 * g], b4[0]), lin_val(a3[b][mb][4 * g + 1], b4[1]),
                                     lin_val(a3[b][mb][4 * g + 2], b4[2]), lin_val(a3[b][mb][4 * g + 3], b4[3])};
-                    if constexpr (E3 == E3_QKV) {
+#ifndef LG_FR_ABL
+                    constexpr int kAbl = 0;
+#else
+                    constexpr int kAbl = LG_FR_ABL;  // diagnostic builds: 1 no rotary, 2 no phase-3 stores
+#endif
+                    if constexpr (E3 == E3_QKV && kAbl != 1) {
                         if (cb < 2 * NO) {  // q, k: rotary pairs (d, d + 1) from this row's tables
                             const int rw = 32 * mb + r;  // (tile row; rows past m hold row m - 1's tables)
                             const f16x4 cc = *(__attribute__((address_space(3))) f16x4*)(lds + kCS + rw * kCSP + (c % kD) * 2);
@@ -1290,6 +1295,9 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
                         dst = q3.out[E3 == E3_QKV ? (lr.first ? 0 : 3) + part : (lr.first ? 0 : 1) + 2 * part] + lr.off +
                               cb % kD + 16 * half;
                     }
+#ifdef LG_FR_ABL
+                    if (LG_FR_ABL == 2) dst = nullptr;
+#endif
                     if (dst) {
                         *reinterpret_cast<f16x8*>(dst) = v0;
                         *reinterpret_cast<f16x8*>(dst + 8) = v1;
