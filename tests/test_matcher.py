@@ -932,3 +932,44 @@ def test_fp16_head_and_inputs_kernels(pairs, m, n):
     err = float((got - ref).abs().max())
     print(f"dual log-softmax f16 P={pairs} {m}x{n}: max-abs {err:.3e}")
     assert err <= 2e-4 * max(1.0, float(ref.abs().max()) / 16)
+
+
+# Random shapes through the chained fp16 forward (round 6): the 16-row FFN kernel with and without its
+# split projection, the 32 / 64-row kernels, ragged row counts (partial tiles, images of a few rows,
+# pairs whose rows cross tiles), every chain kind's fused projection and the two-launch head — against
+# the same fp16 model with the framework's ops around our attention (glue='torch', one pair at a time),
+# every element, at the batched-vs-single bound (two fp16 forwards' rounding spread).
+RANDOM_SHAPES = int(os.environ.get("LG_RANDOM_SHAPES", "12"))  # (LG_RANDOM_SHAPES=n widens it, one-off)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(RANDOM_SHAPES))
+def test_matcher_random_shapes_chained_vs_torch_glue(case):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from lightglue_amd import matcher
+
+    rng = np.random.default_rng(9000 + case)
+    pairs = int(rng.choice([1, 1, 1, 2, 3, 5]))
+    n0 = int(rng.choice([int(rng.integers(1, 64)), int(rng.integers(64, 1100)), int(rng.integers(1100, 2049))],
+                        p=[0.2, 0.6, 0.2]))
+    n1 = 8 * int(rng.integers(1, 256))  # (the fp16 head kernel takes n1 % 8 == 0)
+    dev, dt = torch.device("cuda:0"), torch.float16
+    sd = matcher.seeded_state_dict(7, 9)
+    outs = {}
+    for glue in ("hip", "torch"):
+        m = matcher.LightGlueMatcher(n_layers=9, glue=glue).eval()
+        m.load_state_dict(sd, strict=True)
+        m = m.to(dev, dt)
+        ps = [matcher.synthetic_pair(500 + 13 * case + i, n0, n1) for i in range(pairs)]
+        batch = tuple(torch.cat([p[j] for p in ps], 0).to(dev, dt) for j in range(4))
+        with torch.no_grad():
+            outs[glue] = m(*batch)
+    torch.cuda.synchronize()
+    tol_d, tol_s = BATCHED_VS_SINGLE["float16"]
+    (d0, d1, sc), (r0, r1, rs) = outs["hip"], outs["torch"]
+    assert sc.shape == (pairs, n0, n1) and torch.isfinite(sc).all()
+    ed = max(float((d0 - r0).abs().max()), float((d1 - r1).abs().max()))
+    es = float((sc - rs).abs().max())
+    print(f"random shape {case}: P={pairs} {n0}x{n1} rows {pairs * (n0 + n1)}: desc {ed:.3e} scores {es:.3e}")
+    assert ed <= tol_d and es <= tol_s, (pairs, n0, n1, ed, es)
