@@ -66,9 +66,11 @@ def _check(got, ref, scale, tag, v):
         bound = REG_ABS * scale + ref.abs() * 2.0 ** -11
     else:
         bound = torch.full_like(ref, REG_ABS * scale)
-    # fewer than one 64-key tile: the fp16 rounding of each P (2^-11 relative) no longer averages
-    # out over many keys, so a row's error reaches 2^-11 max|v - o| (observed 1.6e-3 at nkv = 2)
-    if v.shape[2] < 64:
+    # fewer than one 64-key tile, or peaked rows (logit scale >= 2: a row's mass on a few keys): the fp16
+    # rounding of each P (2^-11 relative) no longer averages out over many keys, so a row's error
+    # reaches 2^-11 max|v - o| (observed 1.6e-3 at nkv = 2; 5.1e-3 on the streaming kernel at scale 3,
+    # 24 x 513 x 70 — seed 484 of the 600-case sweep, round 6 — within the 1e-2 contract)
+    if v.shape[2] < 64 or scale >= 2.0:
         bound = bound + 2.0 ** -10 * float(v.double().abs().max())
     excess = float((d - bound).max())
     assert excess <= 0, (tag, f"regression excess {excess:.3e}, max-abs {float(d.max()):.3e}")
