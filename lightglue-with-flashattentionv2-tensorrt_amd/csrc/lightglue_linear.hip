@@ -910,6 +910,11 @@ struct Proj3 {
     f16* out[6];        // SPLIT2: a0 a1 b0 b1; QKV: q0 k0 v0 q1 k1 v1 (per-image head-major); PLAIN: [m, n_store]
     int n_store;        // E3_PLAIN: channels stored per row (the first n_store of 32 NB3 8)
 };
+// The A tile in two halves (LG_FFN_AHALF, default 1; 0: one tile wait, round 6's first form): the
+// x half's loads first, phase 1's first 256 k on it, the heads half written to LDS halfway through.
+#ifndef LG_FFN_AHALF
+#define LG_FFN_AHALF 1
+#endif
 // The weight stream's wave sync (A/B, -DLG_FFN_SYNC=<pieces>): a workgroup barrier every that many
 // 1-KiB pieces per wave inside each phase, so that no wave runs ahead of the others' streams. The
 // waves of a workgroup finish phase 1 ~3.8 k cycles apart (stamps: the LayerNorm's first barrier
@@ -980,18 +985,36 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
 
     // ---- A tile: row 8 i + wave, 16-B unit `lane` (x: units 0..31, head h of the attention output:
     // units 32 + 8 h .. + 7), loaded whole-row coalesced; rows past m repeat row m - 1 ----
-    f16x8 av[4 * MB];
+    // LG_FFN_AHALF (32-row tiles; the 64-row form measured 45.6 -> 47.6 us with it at P = 16): the x half
+    // first, then the heads half — row 16 i + 2 w + lane / 32, unit lane % 32 of each; phase 1's first
+    // half (k < 256) runs on x while the heads land
+    constexpr bool AH = LG_FFN_AHALF && MB == 1;
+    f16x8 av[AH ? 1 : 4 * MB], ax[2 * MB], ac[2 * MB];
+    if constexpr (AH) {
 #pragma unroll
-    for (int i = 0; i < 4 * MB; ++i) {
-        const int grow = min(m0 + 8 * i + wave, p.m - 1);
-        const f16* src;
-        if (lane < 32) {
-            src = p.a + (size_t)grow * (K / 2) + lane * 8;
-        } else {
-            const LinRow lr = lin_row(p, grow, (lane - 32) >> 3);
-            src = (lr.first ? p.ctx0 : p.ctx1) + lr.off + ((lane - 32) & 7) * 8;
+        for (int i = 0; i < 2 * MB; ++i) {
+            const int grow = min(m0 + 16 * i + 2 * wave + (lane >> 5), p.m - 1);
+            ax[i] = *reinterpret_cast<const f16x8*>(p.a + (size_t)grow * (K / 2) + (lane & 31) * 8);
         }
-        av[i] = *reinterpret_cast<const f16x8*>(src);
+#pragma unroll
+        for (int i = 0; i < 2 * MB; ++i) {
+            const int grow = min(m0 + 16 * i + 2 * wave + (lane >> 5), p.m - 1);
+            const LinRow lr = lin_row(p, grow, (lane & 31) >> 3);
+            ac[i] = *reinterpret_cast<const f16x8*>((lr.first ? p.ctx0 : p.ctx1) + lr.off + (lane & 7) * 8);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4 * MB; ++i) {
+            const int grow = min(m0 + 8 * i + wave, p.m - 1);
+            const f16* src;
+            if (lane < 32) {
+                src = p.a + (size_t)grow * (K / 2) + lane * 8;
+            } else {
+                const LinRow lr = lin_row(p, grow, (lane - 32) >> 3);
+                src = (lr.first ? p.ctx0 : p.ctx1) + lr.off + ((lane - 32) & 7) * 8;
+            }
+            av[i] = *reinterpret_cast<const f16x8*>(src);
+        }
     }
     // the epilogue vectors: b1 / gamma / beta (64 units each) and b2 (32 units)
     f16x8 pv = {};
@@ -1037,10 +1060,21 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
         return w;
     };
     // A and the vectors into LDS (the compiler's wait counts the weight loads issued after them)
+    auto put_half = [&](const f16x8 (&hv)[2 * MB], int u0) {
 #pragma unroll
-    for (int i = 0; i < 4 * MB; ++i) {
-        const int row = 8 * i + wave;
-        *(lds_f16x8*)(lds + kA + row * 1024 + ((lane ^ (row & 15)) << 4)) = av[i];
+        for (int i = 0; i < 2 * MB; ++i) {
+            const int row = 16 * i + 2 * wave + (lane >> 5), u = u0 + (lane & 31);
+            *(lds_f16x8*)(lds + kA + row * 1024 + ((u ^ (row & 15)) << 4)) = hv[i];
+        }
+    };
+    if constexpr (AH) {
+        put_half(ax, 0);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4 * MB; ++i) {
+            const int row = 8 * i + wave;
+            *(lds_f16x8*)(lds + kA + row * 1024 + ((lane ^ (row & 15)) << 4)) = av[i];
+        }
     }
     if (tid < 224) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
 #pragma unroll
@@ -1075,6 +1109,13 @@ __global__ __launch_bounds__(512, 1) void ffn_rows_kernel(LinArgs p, const f16* 
 #pragma unroll
     for (int j = 0; j < NS1; ++j) {
         const f16x8 wa = take(2 * j), wb = take(2 * j + 1);
+        if constexpr (AH) {
+            if (j + 1 == NS1 / 2) {  // the heads half into LDS before step NS1 / 2's fragments are read
+                put_half(ac, 32);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+        }
         const BF an = j + 1 < NS1 ? bfrag(kA, j + 1) : af;
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb) {
@@ -1378,6 +1419,16 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
 
     // ---- A tile (two 16-B units a thread: row f / 64, unit f % 64), the vectors; rows past m repeat
     // row m - 1 ----
+#if LG_FFN_AHALF
+    // (row tid / 32: its x unit tid % 32 first, then its heads unit; phase 1's first half runs on x)
+    f16x8 ax, ac;
+    {
+        const int grow = min(m0 + (tid >> 5), p.m - 1);
+        ax = *reinterpret_cast<const f16x8*>(p.a + (size_t)grow * (K / 2) + (tid & 31) * 8);
+        const LinRow lr = lin_row(p, grow, (tid & 31) >> 3);
+        ac = *reinterpret_cast<const f16x8*>((lr.first ? p.ctx0 : p.ctx1) + lr.off + (tid & 7) * 8);
+    }
+#else
     f16x8 av[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -1392,6 +1443,7 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         }
         av[i] = *reinterpret_cast<const f16x8*>(src);
     }
+#endif
     f16x8 pv = {};
     if (tid < 224) {
         const f16* const pvs = tid < 64 ? p.bias : tid < 128 ? gamma : tid < 192 ? beta : b2;
@@ -1430,11 +1482,15 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         if (i + R < NPS) w_[i % R] = piece(i + R);
         return w;
     };
+#if LG_FFN_AHALF
+    *(lds_f16x8*)(lds + kA + tile_unit(tid >> 5, tid & 31)) = ax;
+#else
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int f = 512 * i + tid;
         *(lds_f16x8*)(lds + kA + tile_unit(f >> 6, f & 63)) = av[i];
     }
+#endif
     if (tid < 224) *(lds_f16x8*)(lds + kPar + tid * 16) = pv;
     if (tid < NVB) {
         *(lds_f16x8*)(lds + kB3 + tid * 16) = v3;
@@ -1454,6 +1510,13 @@ __global__ __launch_bounds__(512, 1) void ffn_rows16_kernel(LinArgs p, const f16
         f16x8 w4[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b) w4[b] = take(4 * s + b);
+#if LG_FFN_AHALF
+        if (s + 1 == 8) {  // the heads half into LDS before step 8's fragments are read
+            *(lds_f16x8*)(lds + kA + tile_unit(tid >> 5, 32 + (tid & 31))) = ac;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+#endif
         const f16x8 bn = s + 1 < 16 ? *(lds_f16x8*)(lds + kA + tile_unit(r, 4 * (s + 1) + q)) : bf;
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(w4[b], bf, acc[b], 0, 0, 0);
