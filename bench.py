@@ -177,18 +177,19 @@ def timed_region(run_steps, barrier, sync, reduce_max):
 
 
 def timed_replays(torch, replay, stream, barrier, reduce_max, replays, local=None):
-    """The headline's timed region: barrier + synchronize, then `replays` replays of the K-step
-    graph back to back on the launch stream with a HIP event pair around each (events on the stream
-    the kernels run on), synchronize + barrier. Returns (max over ranks of the median replay time,
+    """The headline's timed region: barrier + synchronize, then `replays` repetitions of the K steps
+    (`replay()`: K plugin enqueues, or one replay of a K-step graph) back to back on the launch
+    stream with a HIP event pair around each (events on the stream the kernels run on),
+    synchronize + barrier. Returns (max over ranks of the median replay time,
     max over ranks of the host wall time per replay), in seconds; `local` (a dict), if given,
     receives this rank's own median under "median_s".
 
     The event pair times exactly the K steps on the GPU. A sleep kernel queued ahead of the replays
     holds the stream while the host submits them (sized from an untimed rehearsal of the host's
-    submission time), so the GPU runs them back to back: the host's graph-launch cost at a short K
-    (~0.1 ms per 20-node replay here, about the GPU time of the 20 calls) stays out of the events
+    submission time), so the GPU runs them back to back: the host's submission cost (~10 us per
+    enqueue here, twice a call's GPU time; ~0.1 ms per 20-node graph replay) stays out of the events
     instead of starving the GPU between calls. The second value is the host's own submission time
-    per replay (launch + two event records), measured around the submission loop alone: the sleep
+    per repetition (the K steps + two event records), measured around the submission loop alone: the sleep
     kernel's artificial backlog is not in it."""
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(replays)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(replays)]
@@ -845,7 +846,10 @@ def main():
     ap.add_argument("--only", choices=["call", "batched"], default=None,
                     help="profiling driver: launch just this workload --steps times (eager), print nothing else")
     ap.add_argument("--replays", type=int, default=0,
-                    help="replays of the K-step graph in the timed region (median taken; 0: enough for ~20k calls)")
+                    help="replays of the K steps in the timed region (median taken; 0: enough for ~20k calls)")
+    ap.add_argument("--launch", choices=["enqueue", "graph"], default="enqueue",
+                    help="how the K timed steps are issued: K plugin enqueues straight onto the stream, or one "
+                         "replay of a graph captured from those K enqueues")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -897,24 +901,34 @@ def main():
             lightglue_amd.mha_hd64(q, k, v, out=out)
     stream.synchronize()
 
-    # Capture the K timed steps (K independent enqueues) into one graph.
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, stream=stream):
+    with torch.cuda.stream(stream):                  # the plugin's enqueue with its bindings prepared once
+        enqueue = lightglue_amd.plugin.bound_enqueue(q, k, v, out)
+
+    def enqueue_steps():                             # the K timed steps: K independent plugin enqueues
         for _ in range(args.steps):
-            lightglue_amd.mha_hd64(q, k, v, out=out)
-    graph.replay()                                   # upload / first-replay cost outside the timer
-    stream.synchronize()
+            enqueue()
+
+    if args.launch == "graph":                       # ... or one replay of a graph captured from them
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            enqueue_steps()
+        graph.replay()                               # upload / first-replay cost outside the timer
+        stream.synchronize()
+        run_steps = graph.replay
+    else:
+        run_steps = enqueue_steps
 
     replays = args.replays if args.replays > 0 else max(10, min(250, -(-5000 // args.steps)))
     mine = {}
-    elapsed, wall = timed_replays(torch, graph.replay, stream, barrier, reduce_max, replays, local=mine)
+    elapsed, wall = timed_replays(torch, run_steps, stream, barrier, reduce_max, replays, local=mine)
     total_calls = args.steps * ws
     value = total_calls / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
     rank_values = gather(dist, round(args.steps / mine["median_s"], 1))  # each rank's own rate
-    # Each replay of a K-step graph pays a fixed ~9 us of graph launch + ~4.8 us for its event pair
-    # on the GPU (tools/timing_probe.py, profiles/r02/timing_probe.txt); at the driver's K = 20
-    # that is ~10 % of the step time. The same calls in 2000-step graphs, for comparison:
+    # Each timed repetition pays ~4.8 us for its event pair on the GPU, and a K-step graph replay a
+    # further ~6-9 us of graph launch (tools/timing_probe.py, profiles/r02/timing_probe.txt): at the
+    # driver's K = 20 the enqueue form runs 5.0 us per call, the graph form 5.35
+    # (profiles/r06/headline_launch_ab.txt). The same calls in 2000-step graphs, for comparison:
     long_rate = None
     if args.steps < 2000:
         g2 = torch.cuda.CUDAGraph()
@@ -959,8 +973,9 @@ def main():
         # an image pair is 36 such calls (9 layers x 2 self + 2 cross), so the
         # attention-only pair rate of the whole job is value / 36 (matcher_e2e_fp16 times whole pairs)
         "attention_pairs_per_s": round(value / 36, 1),
-        "timing": {"replays": replays, "per_replay": "HIP events on the launch stream around one replay of the "
-                                                     "K-step graph; median over replays, max over ranks; replays "
+        "timing": {"replays": replays, "launch": args.launch,
+                   "per_replay": "HIP events on the launch stream around the K steps (K enqueues or one K-step "
+                                 "graph replay); median over replays, max over ranks; replays "
                                                      "queued behind a sleep kernel so host submission does not gap "
                                                      "the GPU",
                    "host_submit_ms_per_replay": round(wall * 1e3, 4),
@@ -968,7 +983,7 @@ def main():
         "per_rank_calls_per_s": rank_values,
         "outputs_bitwise_identical_across_ranks": len(set(digests)) == 1,
         "config": {"workload": "MHAHeadDim64 plugin enqueue, Q/K/V [1,4,1024,64] fp16 -> O fp16 "
-                               "(BASELINE configs[1]); K independent calls per step-graph",
+                               "(BASELINE configs[1]); K independent plugin enqueues per timed repetition",
                    "batch": 1, "heads": 4, "nq": nq, "nkv": nkv, "head_dim": 64,
                    "parallelism": f"replicas{ws}", "pairs": "one pair stream per GPU, no collective",
                    "plan": {"q_waves": q_waves, "kv_waves": kv_waves, "kv_splits": splits}},

@@ -266,6 +266,33 @@ def mha_hd64(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor, out: t
     return out
 
 
+def bound_enqueue(query: torch.Tensor, key: torch.Tensor, value: torch.Tensor, out: torch.Tensor):
+    """The enqueue() of mha_hd64 with its bindings prepared once, as a TensorRT execution context
+    holds them between inferences: descriptors, pointer arrays, workspace and stream are fixed here
+    (the current stream at bind time), and each call of the returned function is one C-ABI
+    mha_hd64_enqueue of the plugin (lightglue_attention_plugin.cpp's enqueue) and nothing else."""
+    _require_gpu(query, key, value)
+    for t in (query, key, value, out):
+        if not t.is_contiguous():
+            raise PluginError("bound_enqueue needs contiguous tensors")
+    plugin = get_plugin()
+    in_desc = [tensor_desc(query), tensor_desc(key), tensor_desc(value)]
+    out_desc = [tensor_desc(out)]
+    stream = torch.cuda.current_stream(query.device).cuda_stream
+    ws = _workspace(query.device, stream, plugin.get_workspace_size(in_desc, out_desc))
+    args = (plugin._h, _desc_array(in_desc), _desc_array(out_desc),
+            (ctypes.c_void_p * 3)(query.data_ptr(), key.data_ptr(), value.data_ptr()),
+            (ctypes.c_void_p * 1)(out.data_ptr()), ws.data_ptr(), stream)
+    fn = plugin._lib.mha_hd64_enqueue
+
+    def enqueue() -> None:
+        status = fn(*args)
+        if status != _lib.STATUS_SUCCESS:
+            _check(status, "enqueue")
+    enqueue.keep = (query, key, value, out, ws)      # the bound buffers outlive the closure's users
+    return enqueue
+
+
 _LAUNCHERS = {
     (torch.float16, torch.float16): "mha_hd64_launch_fp16in_fp16out",
     (torch.float16, torch.float32): "mha_hd64_launch_fp16in_fp32out",

@@ -341,6 +341,32 @@ def test_graph_capture_replay(dev):
     assert torch.equal(out, eager)
 
 
+def test_bound_enqueue_matches_plugin_call(dev):
+    """bench.py's timed steps: the plugin's enqueue with bindings prepared once gives the bits of
+    mha_hd64(), on the stream it was bound on, eagerly and under graph capture."""
+    from lightglue_amd import mha_hd64, plugin, synth
+
+    qn, kn, vn = synth.qkv(11, 1024, 1024)
+    q, k, v = (_t(x, dev, torch.float16) for x in (qn, kn, vn))
+    ref = mha_hd64(q, k, v).clone()
+    out = torch.empty_like(q)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        step = plugin.bound_enqueue(q, k, v, out)
+        for _ in range(3):
+            step()
+    s.synchronize()
+    assert torch.equal(out, ref)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        step()
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
 def test_attention_module_and_autograd_function(dev):
     from lightglue_amd import Attention, MHAHeadDim64, synth
 

@@ -27,7 +27,7 @@ for step in "$@"; do
         tests)  run 900 "tests_${arg//[^a-zA-Z0-9_]/_}.log" python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${arg:+-k "$arg"} || exit $? ;;
         gpu)    run 1100 gpu_suite.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit $? ;;
         ffn_ab) run 600 "ffn_ab.log" python -u tools/ffn_ab.py $arg || exit $? ;;
-        bench)  run 900 "bench.log" python -u bench.py $arg || exit $? ;;
+        bench)  b=${arg//[^a-zA-Z0-9]/_}; run 900 "bench${b:+_${b:0:60}}.log" python -u bench.py $arg || exit $? ;;
         tool)   # one diagnostic script of tools/ (its stdout in <name>.log)
             read -r -a ta <<< "$arg"; tn=${ta[0]}; sfx=$(basename -a "${ta[@]:1}" 2>/dev/null | tr -c 'a-zA-Z0-9\n' '_' | tr '\n' '_')
             run 600 "${tn}_${sfx:0:60}.log" python -u "tools/${tn}.py" "${ta[@]:1}" || exit $? ;;
