@@ -1,5 +1,6 @@
 #!/bin/bash
-# A/B of assign_lse_kernel's block order (LG_ASSIGN_XCD=0 grid order / 1 XCD-contiguous): the
+# A/B of assign_lse_kernel's block order (LG_ASSIGN_XCD=0 grid order / 1 XCD-contiguous; the option existed only in
+# the round-6 A/B build, measured and dropped: profiles/r06/assign_xcd_order_ab.txt). The steps:
 # assignment-head tests, matcher forwards at P = 1 / 16 (interleaved), and a kernel trace each way.
 #   bash tools/gpu/assign_xcd_ab.sh <tag>
 set -o pipefail
