@@ -53,7 +53,10 @@ __global__ __launch_bounds__(NT) void stream_kernel(const u32x4* K, const u32x4*
 
 // The same volume by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB per instruction) into a 16 KiB
 // per-wave LDS region (overwritten in turn: only the transfer rate is of interest).
-template <int KPW, int NT = 512>
+// ROT (round 6): 0 every workgroup issues its pieces in the same order; 1 rotated by the workgroup's
+// index within its head (piece (i + local) % N first), so the head's workgroups start on different
+// lines; 2 rotated by whole 64-key tiles ((local % 4) tiles), the order a kernel could use.
+template <int KPW, int NT = 512, int ROT = 0>
 __global__ __launch_bounds__(NT) void dma_kernel(const u32x4* K, const u32x4* V, u32x4* O, int span) {
     __shared__ __attribute__((aligned(16))) char lds[8 * 16384];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -66,14 +69,16 @@ __global__ __launch_bounds__(NT) void dma_kernel(const u32x4* K, const u32x4* V,
     const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc((void*)(K + (size_t)head * 1024 * 8), (short)0, 1 << 17, 0x00020000);
     const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc((void*)(V + (size_t)head * 1024 * 8), (short)0, 1 << 17, 0x00020000);
     constexpr int N = KPW / 8;  // 1 KiB pieces per tensor
+    const int rot = ROT == 1 ? local % N : ROT == 2 ? (local % 4) * (N / 4) : 0;
+    const unsigned ko = (unsigned)(key0 * 128 + lane * 16);
 #pragma unroll
     for (int i = 0; i < N; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(kr, (__attribute__((address_space(3))) void*)(lds + wave * 16384 + (i & 15) * 1024), 16,
-                                                 (unsigned)(key0 * 128 + lane * 16), i * 1024, 0, 0);
+                                                 ko + (unsigned)(((i + rot) % N) * 1024), 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < N; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(vr, (__attribute__((address_space(3))) void*)(lds + wave * 16384 + ((i + N) & 15) * 1024), 16,
-                                                 (unsigned)(key0 * 128 + lane * 16), i * 1024, 0, 0);
+                                                 ko + (unsigned)(((i + rot) % N) * 1024), 0, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     O[(size_t)blockIdx.x * NT + threadIdx.x] = *(const u32x4*)(lds + threadIdx.x * 16);
@@ -209,6 +214,14 @@ int main() {
            time_graph([&] { dma_kernel<256, 256><<<128, 256, 0, s>>>(K, V, O, 1024); }, s, C));
     printf(", \"dma_nosplit16_256x256_kpw256_us\": %.3f",
            time_graph([&] { dma_kernel<256, 256><<<256, 256, 0, s>>>(K, V, O, 1024); }, s, C));
+    printf(", \"dma_nosplit16_256x256_kpw256_rot_piece_us\": %.3f",
+           time_graph([&] { dma_kernel<256, 256, 1><<<256, 256, 0, s>>>(K, V, O, 1024); }, s, C));
+    printf(", \"dma_nosplit16_256x256_kpw256_rot_tile_us\": %.3f",
+           time_graph([&] { dma_kernel<256, 256, 2><<<256, 256, 0, s>>>(K, V, O, 1024); }, s, C));
+    printf(", \"dma_nosplit16_256x256_kpw256_again_us\": %.3f",
+           time_graph([&] { dma_kernel<256, 256><<<256, 256, 0, s>>>(K, V, O, 1024); }, s, C));
+    printf(", \"dma_nosplit16_256x256_kpw256_rot_piece_again_us\": %.3f",
+           time_graph([&] { dma_kernel<256, 256, 1><<<256, 256, 0, s>>>(K, V, O, 1024); }, s, C));
     printf(", \"dma32_nosplit16_256x256_kpw256_us\": %.3f",
            time_graph([&] { dma32_kernel<256><<<256, 256, 0, s>>>(K, V, O, 1024); }, s, C));
     printf(", \"cvt32_nosplit16_256x256_kpw256_us\": %.3f",
