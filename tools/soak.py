@@ -2,10 +2,12 @@
 stays bitwise equal to the first one computed. Rotates through (a) 1000 headline plugin enqueues
 (1x4x1024^2 fp16, bindings prepared once), (b) the batched launcher at 8 calls (streaming or
 single-pass kernel by the planner), (c) the fp16 matcher forward at P = 1 and P = 16 pairs (graph
-replays), (d) two streams of headline calls with separate workspaces. A progress line every ~30 s,
-one JSON line at the end; exit status 1 on any mismatch.
+replays), (d) two streams of headline calls with separate workspaces; with "full" also (e) the
+plugin's Float path, (f) grouped launches of four ragged calls, (g) four streams under the
+concurrency hint 4, (h) the fp32 matcher at P = 1. A progress line every ~30 s, one JSON line at the
+end; exit status 1 on any mismatch.
 
-    python tools/soak.py [seconds=480]
+    python tools/soak.py [seconds=480] [basic|full]
 """
 import hashlib
 import json
@@ -17,7 +19,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "lightglue-with-flashattentionv2-tensorrt_amd")]
 import torch  # noqa: E402
 
-from lightglue_amd import matcher, mha_hd64_batched, plugin, synth  # noqa: E402
+from lightglue_amd import matcher, mha_hd64_batched, mha_hd64_grouped, plugin, set_concurrency_hint, synth  # noqa: E402
 
 
 def digest(*ts):
@@ -29,6 +31,7 @@ def digest(*ts):
 
 def main():
     seconds = float(sys.argv[1]) if len(sys.argv) > 1 else 480.0
+    full = len(sys.argv) > 2 and sys.argv[2] == "full"
     dev = torch.device("cuda:0")
     st, st2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     q, k, v = (torch.from_numpy(x).to(dev).half().contiguous() for x in synth.qkv(21, 1024, 1024))
@@ -43,17 +46,36 @@ def main():
     model.load_state_dict(matcher.seeded_state_dict(7, 9), strict=True)
     model = model.to(dev, torch.float16)
     graphs = {}
-    for P in (1, 16):
+
+    def capture(key, mdl, P, dt):
         ps = [matcher.synthetic_pair(80 + i, 1024, 1024) for i in range(P)]
-        batch = tuple(torch.cat([p[j] for p in ps], 0).to(dev, torch.float16) for j in range(4))
+        batch = tuple(torch.cat([p[j] for p in ps], 0).to(dev, dt) for j in range(4))
         with torch.no_grad(), torch.cuda.stream(st):
             for _ in range(2):
-                model(*batch)
+                mdl(*batch)
             st.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=st):
-                res = model(*batch)
-        graphs[P] = (g, batch, res)
+                res = mdl(*batch)
+        graphs[key] = (g, batch, res, P)
+
+    capture("P1", model, 1, torch.float16)
+    capture("P16", model, 16, torch.float16)
+    if full:
+        model32 = matcher.LightGlueMatcher(n_layers=9).eval()
+        model32.load_state_dict(matcher.seeded_state_dict(7, 9), strict=True)
+        capture("fp32_P1", model32.to(dev, torch.float32), 1, torch.float32)
+        q32, k32, v32 = (t.float().contiguous() for t in (q, k, v))
+        o32 = torch.empty_like(q32)
+        with torch.cuda.stream(st):
+            call32 = plugin.bound_enqueue(q32, k32, v32, o32)
+        ragged = [(600, 1000), (1000, 600), (333, 777), (1024, 1024)]
+        gcalls = [tuple(torch.from_numpy(x).to(dev).half().contiguous() for x in synth.qkv(30 + i, a, b))
+                  for i, (a, b) in enumerate(ragged)]
+        gouts = [torch.empty_like(c[0]) for c in gcalls]
+        hst = [torch.cuda.Stream(dev) for _ in range(4)]
+        hq = [tuple(torch.from_numpy(x).to(dev).half().contiguous() for x in synth.qkv(40 + i, 1024, 1024)) for i in range(4)]
+        ho = [torch.empty_like(t[0]) for t in hq]
 
     def work(name):
         if name == "headline":
@@ -76,15 +98,39 @@ def main():
             st.synchronize()
             st2.synchronize()
             return digest(out, out2), 1000
-        P = int(name[1:])
-        g, _, res = graphs[P]
+        if name == "float_path":
+            with torch.cuda.stream(st):
+                for _ in range(500):
+                    call32()
+            st.synchronize()
+            return digest(o32), 500
+        if name == "grouped_ragged":
+            with torch.cuda.stream(st):
+                for _ in range(200):
+                    mha_hd64_grouped(gcalls, outs=gouts)
+            st.synchronize()
+            return digest(*gouts), 200 * len(gcalls)
+        if name == "hint4":
+            prev = set_concurrency_hint(4)
+            try:
+                for i, s_ in enumerate(hst):
+                    with torch.cuda.stream(s_):
+                        for _ in range(250):
+                            plugin.mha_hd64(*hq[i], out=ho[i])
+                for s_ in hst:
+                    s_.synchronize()
+            finally:
+                set_concurrency_hint(prev)
+            return digest(*ho), 1000
+        g, _, res, P = graphs[name]
         for _ in range(20):
             g.replay()
         st.synchronize()
         ts = list(res.values()) if isinstance(res, dict) else list(res)
         return digest(*[t for t in ts if torch.is_tensor(t)]), 20 * P
 
-    names = ["headline", "batched8", "two_streams", "P1", "P16"]
+    names = ["headline", "batched8", "two_streams", "P1", "P16"] + (
+        ["float_path", "grouped_ragged", "hint4", "fp32_P1"] if full else [])
     first, counts, bad = {}, {n: 0 for n in names}, []
     t0 = last = time.time()
     rounds = 0
@@ -101,7 +147,8 @@ def main():
             last = time.time()
             print(json.dumps({"elapsed_s": round(last - t0, 1), "rounds": rounds, "mismatches": len(bad)}), flush=True)
     print(json.dumps({"soak_s": round(time.time() - t0, 1), "rounds": rounds, "units": counts,
-                      "units_meaning": "attention calls (headline, batched8, two_streams) / image pairs (P1, P16)",
+                      "units_meaning": "attention calls (headline, batched8, two_streams, float_path, grouped_ragged, "
+                                       "hint4) / image pairs (P1, P16, fp32_P1)",
                       "digests": first, "mismatches": bad, "ok": not bad}), flush=True)
     sys.exit(1 if bad else 0)
 
